@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py -- HPACK Huffman encode+decode, device-resident, batched headers.
+
+Metric (BASELINE.json): "GB/s HPACK Huffman enc+dec (device-resident,
+batched headers); %HBM roofline".  One step = one batched encode of the
+rank's synthetic header strings (count -> scan -> pack, the emit_string
+pair lib/nghttp2_hd.c:1009/:1037) followed by one batched decode of the
+result (slots -> nibble-FSM decode with final=1, hd_inflate_read_huff
+lib/nghttp2_hd.c:1728-1751).  Inputs are resident in HBM before timing.
+
+value = sum over ranks of the algorithmic bytes B = 2R + 2E + 24 per string
+ / max-over-ranks wall time of the K timed steps.
+Multi-GPU: independent batches per rank (weak scaling), no collective on the
+data path; the only collectives are the timing barrier and the max.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CONFIG_NAMES = {
+    2: "1M short pseudo-header strings (8-64 B), encode+decode, 1xMI355X",
+    3: "1M mixed-length header values (16-1024 B, Zipf), encode+decode, 1xMI355X",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3])
+    ap.add_argument("--strings", type=int, default=1 << 20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--host-resident", action="store_true",
+                    help="also time the pinned-host H2D+D2H round trip")
+    return ap.parse_args()
+
+
+def cpu_cores_available():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(pool, off, threads):
+    """Oracle (port of lib/nghttp2_hd_huffman.c) timed on host cores:
+    count+encode then decode(final=1), best of repeats; same B accounting."""
+    from oracle import oracle as O
+    n = len(off) - 1
+    raw = int(off[-1])
+    res = {}
+    for nth in sorted({1, threads}):
+        best = None
+        reps = 3 if nth == 1 else 5
+        for _ in range(reps + 1):  # first rep is the warm-up
+            te, td, etot, st = O.roundtrip_timed(pool, off, nth)
+            assert (st >= 0).all()
+            t = te + td
+            best = t if best is None or t < best else best
+        B = 2 * raw + 2 * etot + 24 * n
+        res[nth] = (B / best / 1e9, best)
+    return res
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import nghttp2_amd
+    from nghttp2_amd import workloads as W
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    n = args.strings
+    seed = W.SEED[args.config] + 7919 * rank  # each rank its own batch (weak scaling)
+    if args.config == 2:
+        pool, off = W.gen_pseudo_headers(n, seed=seed)
+    else:
+        pool, off = W.gen_mixed_values(n, seed=seed)
+    raw_bytes = int(off[-1])
+
+    codec = nghttp2_amd.HuffmanBatchCodec(dev)
+    src = torch.from_numpy(pool).to(dev)
+    src_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    enc_cap = codec.encode_bound(raw_bytes, n)
+    enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
+    enc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    dec_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    dec_cap = (enc_cap * 8) // 5 + n + 16
+    dec = torch.empty(dec_cap, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        codec.encode(src, src_off, raw_bytes=raw_bytes, dst=enc, dst_off=enc_off)
+        codec.decode_slots(enc_off, dst_off=dec_off)
+        if i is not None:
+            ev[i][1].record(stream)
+        codec.decode(enc, enc_off, dst_off=dec_off, dst=dec, status=status)
+        if i is not None:
+            ev[i][2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # correctness gate on this rank's batch (fails loudly, never measured)
+    st = status.cpu().numpy()
+    raw_len = np.diff(off.astype(np.int64))
+    assert np.array_equal(st, raw_len), "decode(encode(x)) length mismatch"
+    enc_total = int(enc_off[-1].item())
+    do = dec_off.cpu().numpy().view(np.uint32).astype(np.int64)
+    dh = dec.cpu().numpy()
+    idx = np.repeat(do[:-1], raw_len) + (np.arange(raw_bytes) - np.repeat(off[:-1].astype(np.int64), raw_len))
+    assert np.array_equal(dh[idx], pool[:raw_bytes]), "decode(encode(x)) != x"
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+
+    B_rank = 2 * raw_bytes + 2 * enc_total + 24 * n
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        b = torch.tensor([float(B_rank)], dtype=torch.float64, device=dev)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        B_total = float(b.item())
+    else:
+        B_total = float(B_rank)
+
+    t_enc = np.mean([ev[i][0].elapsed_time(ev[i][1]) for i in range(args.steps)]) * 1e-3
+    t_dec = np.mean([ev[i][1].elapsed_time(ev[i][2]) for i in range(args.steps)]) * 1e-3
+    ms_per_step = elapsed / args.steps * 1e3
+    value = B_total * args.steps / elapsed / 1e9
+
+    # roofline of the dominant kernel (k_decode: one launch per step)
+    dec_alg = raw_bytes + enc_total + 12 * n  # reads E + offsets, writes R + status
+    enc_alg = raw_bytes + enc_total + 12 * n
+    if t_dec >= t_enc:
+        kern, alg, tk = "k_decode", dec_alg, t_dec
+    else:
+        kern, alg, tk = "encode (k_enc_count+k_scan_tiles+k_encode)", enc_alg, t_enc
+    achieved = alg / tk / 1e9
+    roof = {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None, "alg_bytes_per_launch": alg,
+            "launch_ms": round(tk * 1e3, 4), "enc_ms": round(t_enc * 1e3, 4),
+            "dec_ms": round(t_dec * 1e3, 4)}
+
+    out = {"metric": "GB/s HPACK Huffman enc+dec (device-resident, batched headers)",
+           "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (numpy PCG64, seed 0x%X + 7919*rank)" % W.SEED[args.config],
+           "config": {"workload": CONFIG_NAMES[args.config], "strings_per_gpu": n,
+                      "raw_bytes_per_gpu": raw_bytes, "enc_bytes_per_gpu": enc_total,
+                      "E_over_R": round(enc_total / raw_bytes, 4),
+                      "alg_bytes_per_step_all_gpus": int(B_total),
+                      "parallelism": "shard%d (independent batches, no collective)" % world},
+           "roofline": roof}
+
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        threads = max(1, min(args.cpu_threads, cpu_cores_available()))
+        res = cpu_baseline(pool, off, threads)
+        out["cpu_baseline"] = {
+            "value": round(res[threads][0], 4), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": "the same %d-string batch, oracle/huff_oracle.c (restatement of "
+                      "lib/nghttp2_hd_huffman.c, gcc -O2), count+encode+decode(final=1), "
+                      "best of 5 after 1 warm-up, %d pthreads; 1-thread: %.4f GB/s"
+                      % (n, threads, res[1][0]),
+            "value_1thread": round(res[1][0], 4)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

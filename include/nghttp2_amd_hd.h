@@ -1,0 +1,157 @@
+/*
+ * nghttp2_amd_hd.h -- C ABI of the MI355X-native HPACK Huffman engine.
+ *
+ * This is the drop-in boundary for nghttp2's HPACK Huffman hot path
+ * (lib/nghttp2_hd_huffman.c + lib/nghttp2_hd_huffman_data.c in the
+ * reference).  Plain C: pointers, sizes and ints only.  HIP streams are
+ * passed as `void *` (a hipStream_t; NULL = the default stream).
+ *
+ * Two groups of entry points:
+ *
+ *  1. Batched, device-resident API (nghttp2_amd_hd_huff_*_batch).  N
+ *     independent header strings in SoA form: one contiguous byte pool plus
+ *     uint32 offsets[N+1] (string i = pool[off[i] .. off[i+1])).  All
+ *     pointers are device pointers (hipMalloc'd or HBM-resident torch
+ *     storage).  Calls are asynchronous on `stream`.  This is what the
+ *     batched drivers (replacing src/deflatehd.cc / src/inflatehd.cc) and
+ *     an integration under emit_string / hd_inflate_read_huff bind.
+ *
+ *  2. Link-level replacements of the reference's internal Huffman API
+ *     (lib/nghttp2_hd.h:394-440) -- see nghttp2_amd_hd_huffman_compat.h.
+ *
+ * Pool requirements (device API): pool base pointers 16-byte aligned; the
+ * source pool readable up to align_up(off[N], 16) bytes (kernels load
+ * aligned 16-byte words).  Offsets are uint32, so one batch's pool is
+ * < 4 GiB; shard larger sets (multi-GPU).
+ *
+ * Error convention: 0 on success or a negative nghttp2_error code
+ * (lib/includes/nghttp2/nghttp2.h:278-459).  Per-string decode results are
+ * reported in a status array, never by the return value.
+ */
+#ifndef NGHTTP2_AMD_HD_H
+#define NGHTTP2_AMD_HD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* nghttp2_error values used on this path (lib/includes/nghttp2/nghttp2.h) */
+#define NGHTTP2_AMD_ERR_INVALID_ARGUMENT (-501) /* nghttp2.h:278 */
+#define NGHTTP2_AMD_ERR_BUFFER_ERROR (-502)     /* nghttp2.h:282 */
+#define NGHTTP2_AMD_ERR_HEADER_COMP (-523)      /* nghttp2.h:378 */
+#define NGHTTP2_AMD_ERR_FATAL (-900)            /* nghttp2.h:451 (HIP error) */
+#define NGHTTP2_AMD_ERR_NOMEM (-901)            /* nghttp2.h:455 */
+
+/* Decode-context flag bits (lib/nghttp2_hd_huffman.h:35-37). */
+#define NGHTTP2_AMD_HUFF_ACCEPTED 0x01u
+#define NGHTTP2_AMD_HUFF_SYM 0x02u
+/* Failure (EOS decoded) state id (lib/nghttp2_hd_huffman.h:44-48). */
+#define NGHTTP2_AMD_HUFF_FAIL_STATE 0x100u
+
+/* Library version string, e.g. "nghttp2_amd_hd 0.1.0 gfx950". */
+const char *nghttp2_amd_hd_version(void);
+
+/* Copies the engine's Huffman tables out in the reference's struct layouts
+ * so a caller can check them against lib/nghttp2_hd_huffman_data.c without a
+ * GPU: sym_out receives huff_sym_table (257 x {u32 nbits, u32 code} = 2056
+ * bytes, lib/nghttp2_hd_huffman_data.c:29-94), dec_out receives
+ * huff_decode_table (257 x 16 x {u16 fstate, u8 flags, u8 sym} = 16448 bytes,
+ * :96-4980).  Either pointer may be NULL.  Returns 0. */
+int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out);
+
+/* ------------------------------------------------------------------ */
+/* Sizing helpers (host-only, no GPU needed)                           */
+/* ------------------------------------------------------------------ */
+
+/* Upper bound of the encoded pool for `raw_bytes` bytes in `n` strings:
+ * every symbol is at most 30 bits (RFC 7541 App. B), plus one padding byte
+ * per string, rounded up to 16. */
+size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n);
+
+/* Bytes of device workspace nghttp2_amd_hd_huff_encode_batch and
+ * nghttp2_amd_hd_huff_decode_slots need for `n` strings. */
+size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
+
+/* ------------------------------------------------------------------ */
+/* Batched device-resident API                                          */
+/* ------------------------------------------------------------------ */
+
+/*
+ * Encode N strings.  Replaces, for a whole batch, emit_string's
+ * nghttp2_hd_huff_encode_count + nghttp2_hd_huff_encode pair
+ * (lib/nghttp2_hd.c:1009, :1037; lib/nghttp2_hd_huffman.c:34-104).
+ *
+ *   src, src_off[n+1] : raw strings (device)
+ *   dst               : encoded pool (device), >= dst_cap bytes
+ *   dst_off[n+1]      : OUT: encoded string i = dst[dst_off[i]..dst_off[i+1]);
+ *                       dst_off[i+1]-dst_off[i] == nghttp2_hd_huff_encode_count
+ *   workspace         : device scratch, nghttp2_amd_hd_huff_workspace_size(n)
+ *
+ * Output bytes equal lib/nghttp2_hd_huffman.c's, including the EOS-prefix
+ * (all ones) padding of the last byte.  dst_cap must be >=
+ * nghttp2_amd_hd_huff_encode_bound(src_off[n]-src_off[0], n); a smaller
+ * capacity returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT (the kernels never
+ * write past dst_cap).
+ */
+int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
+                                     uint32_t n, uint8_t *dst, size_t dst_cap,
+                                     uint32_t *dst_off, void *workspace,
+                                     size_t workspace_size, void *stream);
+
+/*
+ * Encoded lengths only: enc_len[i] = nghttp2_hd_huff_encode_count(string i)
+ * (lib/nghttp2_hd_huffman.c:34-43).
+ */
+int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src,
+                                           const uint32_t *src_off, uint32_t n,
+                                           uint32_t *enc_len, void *stream);
+
+/*
+ * Output slots for a decode batch: dst_off[i+1]-dst_off[i] =
+ * floor(8*E_i/5)+1, the reference's allocation for a Huffman literal
+ * (nghttp2_huff_estimate_decode_length, lib/nghttp2_hd_huffman.h:76-78,
+ * used at lib/nghttp2_hd.c:2080-2082 / :2166-2168).  dst_off[n] is the
+ * pool size to allocate.
+ */
+int nghttp2_amd_hd_huff_decode_slots(const uint32_t *src_off, uint32_t n,
+                                     uint32_t *dst_off, void *workspace,
+                                     size_t workspace_size, void *stream);
+
+/*
+ * Decode N whole Huffman strings (each call is final, fin=1).  Replaces,
+ * for a batch, hd_inflate_read_huff's nghttp2_hd_huff_decode_context_init +
+ * nghttp2_hd_huff_decode(..., fin=1) + nghttp2_hd_huff_decode_failure_state
+ * (lib/nghttp2_hd.c:1728-1751, :2076, :2162;
+ * lib/nghttp2_hd_huffman.c:106-147).
+ *
+ *   src, src_off[n+1] : encoded strings (device)
+ *   dst, dst_off[n+1] : output slots (device); string i's decoded bytes are
+ *                       written to dst[dst_off[i] ...]
+ *   status[n]         : OUT: decoded length (>= 0), or
+ *                       NGHTTP2_AMD_ERR_HEADER_COMP (-523) exactly when the
+ *                       reference returns it (non-accepting end state,
+ *                       including EOS decoded), or
+ *                       NGHTTP2_AMD_ERR_BUFFER_ERROR (-502) when the slot is
+ *                       smaller than the decoded length.
+ *   fstate[n], flags[n] : OUT, optional (NULL to skip): the final
+ *                       nghttp2_hd_huff_decode_context {fstate, flags}
+ *                       (lib/nghttp2_hd_huffman.h:56-60) after the string;
+ *                       fstate == 0x100 <=> failure_state().
+ *
+ * On -523 the bytes decoded before the failure are still written (as the
+ * reference leaves them in buf), so dst matches the reference byte for byte.
+ */
+int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off,
+                                     uint32_t n, uint8_t *dst,
+                                     const uint32_t *dst_off, int32_t *status,
+                                     uint16_t *fstate, uint8_t *flags,
+                                     void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NGHTTP2_AMD_HD_H */

@@ -1,0 +1,176 @@
+"""ctypes binding of include/nghttp2_amd_hd.h (the engine's C ABI).
+
+HuffmanBatchCodec mirrors, for batches of strings, the reference's internal
+Huffman API (lib/nghttp2_hd.h:385-440):
+
+  ==========================================  ==================================
+  reference (lib/nghttp2_hd_huffman.c)        batched engine call
+  ==========================================  ==================================
+  nghttp2_hd_huff_encode_count  :34-43        encode_count(src, src_off)
+  nghttp2_hd_huff_encode        :45-104       encode(src, src_off)
+  nghttp2_hd_huff_decode_context_init :106    (implicit per string)
+  nghttp2_hd_huff_decode(fin=1) :111-143      decode(src, src_off) -> status
+  nghttp2_hd_huff_decode_failure_state :145   fstate == 0x100
+  nghttp2_huff_estimate_decode_length (.h:76) decode_slots(src_off)
+  ==========================================  ==================================
+
+Tensors are torch CUDA (HIP) tensors: uint8 pools, int32 tensors holding
+uint32 offsets.  Errors follow nghttp2: negative nghttp2_error codes raise
+RuntimeError; per-string decode status is an int32 tensor.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libnghttp2_amd_hd.so"
+
+NGHTTP2_ERR_INVALID_ARGUMENT = -501
+NGHTTP2_ERR_BUFFER_ERROR = -502
+NGHTTP2_ERR_HEADER_COMP = -523
+NGHTTP2_ERR_FATAL = -900
+
+_lib = None
+
+
+def lib_path():
+    return os.path.join(HERE, "lib", LIB_NAME)
+
+
+def lib():
+    """Load the HIP library; raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(
+                "nghttp2_amd: HIP library %s is missing -- run "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % path)
+        L = ctypes.CDLL(path)
+        vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+        L.nghttp2_amd_hd_version.restype = ctypes.c_char_p
+        L.nghttp2_amd_hd_huff_tables.argtypes = [vp, vp]
+        L.nghttp2_amd_hd_huff_encode_bound.restype = sz
+        L.nghttp2_amd_hd_huff_encode_bound.argtypes = [ctypes.c_uint64, u32]
+        L.nghttp2_amd_hd_huff_workspace_size.restype = sz
+        L.nghttp2_amd_hd_huff_workspace_size.argtypes = [u32]
+        L.nghttp2_amd_hd_huff_encode_batch.argtypes = [vp, vp, u32, vp, sz, vp, vp, sz, vp]
+        L.nghttp2_amd_hd_huff_encode_count_batch.argtypes = [vp, vp, u32, vp, vp]
+        L.nghttp2_amd_hd_huff_decode_slots.argtypes = [vp, u32, vp, vp, sz, vp]
+        L.nghttp2_amd_hd_huff_decode_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def tables_ref_layout():
+    """The engine's tables in the reference struct layouts (host-only)."""
+    sym = ctypes.create_string_buffer(257 * 8)
+    dec = ctypes.create_string_buffer(257 * 16 * 4)
+    lib().nghttp2_amd_hd_huff_tables(sym, dec)
+    return sym.raw, dec.raw
+
+
+def _check(rv, what):
+    if rv != 0:
+        raise RuntimeError("nghttp2_amd: %s failed with nghttp2 error %d" % (what, rv))
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class HuffmanBatchCodec:
+    """Batched HPACK Huffman codec on one device.
+
+    Keeps a workspace sized for the largest batch seen; all calls are
+    asynchronous on the given (default: current) torch stream.
+    """
+
+    def __init__(self, device=None):
+        import torch
+        self.torch = torch
+        self.device = torch.device(device if device is not None else "cuda")
+        self.L = lib()
+        self._ws = None
+
+    def _workspace(self, n):
+        need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
+        return self._ws
+
+    def encode_bound(self, raw_bytes, n):
+        return self.L.nghttp2_amd_hd_huff_encode_bound(int(raw_bytes), int(n))
+
+    def encode(self, src, src_off, raw_bytes=None, dst=None, dst_off=None, stream=None):
+        """Encode strings; returns (dst pool, dst_off int32[n+1])."""
+        torch = self.torch
+        n = src_off.numel() - 1
+        if raw_bytes is None:
+            raw_bytes = src.numel()
+        cap = self.encode_bound(raw_bytes, n)
+        if dst is None:
+            dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        if dst_off is None:
+            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+        ws = self._workspace(n)
+        rv = self.L.nghttp2_amd_hd_huff_encode_batch(
+            _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(ws),
+            ws.numel(), _stream(stream))
+        _check(rv, "encode_batch")
+        return dst, dst_off
+
+    def encode_count(self, src, src_off, enc_len=None, stream=None):
+        n = src_off.numel() - 1
+        if enc_len is None:
+            enc_len = self.torch.empty(max(1, n), dtype=self.torch.int32, device=self.device)
+        rv = self.L.nghttp2_amd_hd_huff_encode_count_batch(
+            _p(src), _p(src_off), n, _p(enc_len), _stream(stream))
+        _check(rv, "encode_count_batch")
+        return enc_len[:n]
+
+    def decode_slots(self, src_off, dst_off=None, stream=None):
+        n = src_off.numel() - 1
+        if dst_off is None:
+            dst_off = self.torch.empty(n + 1, dtype=self.torch.int32, device=self.device)
+        ws = self._workspace(n)
+        rv = self.L.nghttp2_amd_hd_huff_decode_slots(
+            _p(src_off), n, _p(dst_off), _p(ws), ws.numel(), _stream(stream))
+        _check(rv, "decode_slots")
+        return dst_off
+
+    def decode(self, src, src_off, dst_off=None, dst=None, dst_cap=None, status=None,
+               want_ctx=False, stream=None):
+        """Decode strings (fin=1 each).  Returns (dst, dst_off, status[, fstate, flags]).
+
+        dst_off defaults to the reference's floor(8E/5)+1 slots; dst_cap must
+        then be given (or is derived from src size: 8*E_total/5 + n + 16).
+        """
+        torch = self.torch
+        n = src_off.numel() - 1
+        if dst_off is None:
+            dst_off = self.decode_slots(src_off, stream=stream)
+            if dst_cap is None:
+                dst_cap = (src.numel() * 8) // 5 + n + 16
+        if dst is None:
+            if dst_cap is None:
+                dst_cap = int(dst_off[-1].item()) + 16
+            dst = torch.empty(dst_cap, dtype=torch.uint8, device=self.device)
+        if status is None:
+            status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        fstate = flags = None
+        if want_ctx:
+            fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
+            flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        rv = self.L.nghttp2_amd_hd_huff_decode_batch(
+            _p(src), _p(src_off), n, _p(dst), _p(dst_off), _p(status), _p(fstate),
+            _p(flags), _stream(stream))
+        _check(rv, "decode_batch")
+        if want_ctx:
+            return dst, dst_off, status[:n], fstate[:n], flags[:n]
+        return dst, dst_off, status[:n]

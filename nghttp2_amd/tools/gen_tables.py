@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Generate the HPACK Huffman device tables (nghttp2_amd/csrc/hd_huff_tables.inc).
+
+The product's tables are derived here from the 257 RFC 7541 Appendix B code
+lengths alone, using canonical-code arithmetic (the RFC code is canonical:
+codes are assigned in (length, symbol) order -- checked against the
+reference's own generator by oracle/pin_reference.py).  This replaces the
+reference's generated data file lib/nghttp2_hd_huffman_data.c and its
+generator mkhufftbl.py with a different derivation that yields the same
+state numbering and transition semantics:
+
+* encode table (ref: huff_sym_table, lib/nghttp2_hd_huffman_data.c:29-94):
+  per symbol {MSB-aligned code, nbits}.
+* nibble FSM (ref: huff_decode_table, lib/nghttp2_hd_huffman_data.c:96-4980;
+  semantics lib/nghttp2_hd_huffman.h:39-52): state = pre-order index of an
+  internal node of the code tree (0 = root, 256 = failure sink); for each
+  4-bit input the entry holds {next state u16, flags u8, sym u8} packed as
+  one little-endian u32: ``fstate | flags << 16 | sym << 24``.
+  flags: 0x01 ACCEPTED (state is the root or an all-ones prefix of <= 7
+  bits), 0x02 SYM (a symbol completed inside the nibble).  Completing EOS
+  (symbol 256) leads to the sink with flags 0.
+* canonical decode helpers for the fast kernels: per code length L the first
+  code (left-justified to 32 bits) and the symbol index base, plus the
+  symbol list sorted in canonical order, and a per-depth map from an internal
+  prefix to its FSM state id so a canonical decoder can report the exact
+  reference state at the end of a string.
+
+Run: python3 nghttp2_amd/tools/gen_tables.py  (rewrites the .inc file).
+"""
+import hashlib
+import os
+import struct
+import sys
+
+# RFC 7541 Appendix B: code length of symbols 0..255 and EOS (256).
+RFC7541_LEN = [
+    13, 23, 28, 28, 28, 28, 28, 28, 28, 24, 30, 28, 28, 30, 28, 28, 28, 28, 28,
+    28, 28, 28, 30, 28, 28, 28, 28, 28, 28, 28, 28, 28, 6, 10, 10, 12, 13, 6,
+    8, 11, 10, 10, 8, 11, 8, 6, 6, 6, 5, 5, 5, 6, 6, 6, 6, 6, 6,
+    6, 7, 8, 15, 6, 12, 10, 13, 6, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7,
+    7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 8, 7, 8, 13, 19, 13, 14,
+    6, 15, 5, 6, 5, 6, 5, 6, 6, 6, 5, 7, 7, 6, 6, 6, 5, 6, 7,
+    6, 5, 5, 6, 7, 7, 7, 7, 7, 15, 11, 14, 13, 28, 20, 22, 20, 20, 22,
+    22, 22, 23, 22, 23, 23, 23, 23, 23, 24, 23, 24, 24, 22, 23, 24, 23, 23, 23,
+    23, 21, 22, 23, 22, 23, 23, 24, 22, 21, 20, 22, 22, 23, 23, 21, 23, 22, 22,
+    24, 21, 22, 23, 23, 21, 21, 22, 21, 23, 22, 23, 23, 20, 22, 22, 22, 23, 22,
+    22, 23, 26, 26, 20, 19, 22, 23, 22, 25, 26, 26, 26, 27, 27, 26, 24, 25, 19,
+    21, 26, 27, 27, 26, 27, 24, 21, 21, 26, 26, 28, 27, 27, 27, 20, 24, 20, 21,
+    22, 21, 21, 23, 22, 22, 25, 25, 24, 24, 26, 23, 26, 27, 26, 26, 27, 27, 27,
+    27, 27, 28, 27, 27, 27, 27, 27, 26, 30]
+
+ACCEPTED = 0x01
+SYM = 0x02
+FAIL_STATE = 256
+EOS = 256
+
+
+def canonical_codes():
+    """Return (codes, order): codes[s] = (value, length) LSB-aligned."""
+    order = sorted(range(257), key=lambda s: (RFC7541_LEN[s], s))
+    codes = [None] * 257
+    code, prev = 0, RFC7541_LEN[order[0]]
+    for s in order:
+        L = RFC7541_LEN[s]
+        code <<= (L - prev)
+        prev = L
+        codes[s] = (code, L)
+        code += 1
+    return codes, order
+
+
+def build():
+    codes, order = canonical_codes()
+    leaf = {(v, L): s for s, (v, L) in enumerate(codes)}
+    maxlen = max(RFC7541_LEN)
+    # A prefix (v, d) is an internal node iff some code longer than d starts
+    # with it.  Collect internal prefixes, then number them in pre-order
+    # (root, then the 0-subtree, then the 1-subtree).
+    internal = set()
+    for s, (v, L) in enumerate(codes):
+        for d in range(L):
+            internal.add((v >> (L - d), d))
+    ids = {}
+
+    def preorder(v, d):
+        if (v, d) not in internal:
+            return
+        ids[(v, d)] = len(ids)
+        preorder(v << 1, d + 1)
+        preorder((v << 1) | 1, d + 1)
+
+    preorder(0, 0)
+    assert len(ids) == 256, len(ids)
+
+    def accepts(v, d):
+        return d <= 7 and v == (1 << d) - 1
+
+    fsm = [[0] * 16 for _ in range(257)]
+    for (v0, d0), sid in ids.items():
+        for nib in range(16):
+            v, d, sym = v0, d0, None
+            failed = False
+            for k in range(3, -1, -1):
+                v = (v << 1) | ((nib >> k) & 1)
+                d += 1
+                s = leaf.get((v, d))
+                if s is not None:
+                    if s == EOS:
+                        failed = True
+                        # bits after EOS inside the nibble are irrelevant:
+                        # the sink absorbs everything.
+                        break
+                    sym = s
+                    v, d = 0, 0
+            if failed:
+                fsm[sid][nib] = FAIL_STATE
+                continue
+            flags = 0
+            if sym is not None:
+                flags |= SYM
+            if d == 0:
+                nxt = 0
+                flags |= ACCEPTED
+            else:
+                nxt = ids[(v, d)]
+                if accepts(v, d):
+                    flags |= ACCEPTED
+            fsm[sid][nib] = nxt | (flags << 16) | ((sym or 0) << 24)
+    for nib in range(16):
+        fsm[256][nib] = FAIL_STATE
+
+    enc = []
+    for s in range(257):
+        v, L = codes[s]
+        enc.append(((v << (32 - L)) & 0xFFFFFFFF, L))
+
+    # canonical decode helpers: for each length L in 1..30, the first code of
+    # that length left-justified to 32 bits ("limit" style), the count and
+    # the index of its first symbol in canonical order.
+    count = [0] * (maxlen + 2)
+    for s in range(257):
+        count[RFC7541_LEN[s]] += 1
+    first = [0] * (maxlen + 2)
+    base = [0] * (maxlen + 2)
+    code = 0
+    idx = 0
+    for L in range(1, maxlen + 1):
+        first[L] = code
+        base[L] = idx
+        code = (code + count[L]) << 1
+        idx += count[L]
+    # internal-prefix -> state id, grouped by depth: for depth d the internal
+    # prefixes form the contiguous range [lo_d, 2^d) (canonical code property,
+    # asserted here).
+    depth_lo = [0] * 30
+    depth_base = [0] * 30
+    id_list = []
+    for d in range(30):
+        vs = sorted(v for (v, dd) in internal if dd == d)
+        assert vs == list(range(vs[0], (1 << d))), d
+        depth_lo[d] = vs[0]
+        depth_base[d] = len(id_list)
+        id_list.extend(ids[(v, d)] for v in vs)
+    assert len(id_list) == 256
+    return dict(enc=enc, fsm=fsm, order=order, count=count, first=first,
+                base=base, depth_lo=depth_lo, depth_base=depth_base,
+                id_list=id_list)
+
+
+def packed_ref_layout(t):
+    """Bytes of the tables in the reference's struct layouts (for pinning):
+    huff_sym_table as {u32 nbits; u32 code}, huff_decode_table as
+    {u16 fstate; u8 flags; u8 sym}, both little-endian."""
+    sym = b"".join(struct.pack("<II", L, c) for c, L in t["enc"])
+    dec = b"".join(struct.pack("<I", e) for row in t["fsm"] for e in row)
+    return sym, dec
+
+
+def write_inc(t, path):
+    sym, dec = packed_ref_layout(t)
+    lines = []
+    w = lines.append
+    w("/* GENERATED by nghttp2_amd/tools/gen_tables.py -- do not edit. */")
+    w("/* sha256 sym  (ref layout): %s */" % hashlib.sha256(sym).hexdigest())
+    w("/* sha256 fsm  (ref layout): %s */" % hashlib.sha256(dec).hexdigest())
+    w("#define HD_HUFF_FSM_STATES 257")
+    w("#define HD_HUFF_FAIL_STATE 256")
+    w("/* encode: MSB-aligned code, code length */")
+    w("HD_TBL const unsigned int hd_huff_enc_code[257] = {")
+    for i in range(0, 257, 6):
+        w("  " + ", ".join("0x%08Xu" % c for c, _ in t["enc"][i:i + 6]) + ",")
+    w("};")
+    w("HD_TBL const unsigned char hd_huff_enc_len[257] = {")
+    for i in range(0, 257, 20):
+        w("  " + ", ".join("%d" % L for _, L in t["enc"][i:i + 20]) + ",")
+    w("};")
+    w("/* nibble FSM: fstate | flags << 16 | sym << 24 */")
+    w("HD_TBL const unsigned int hd_huff_fsm[257 * 16] = {")
+    for s, row in enumerate(t["fsm"]):
+        w("  /* %3d */ " % s + ", ".join("0x%08Xu" % e for e in row) + ",")
+    w("};")
+    w("/* canonical order of symbols (by length, then value) */")
+    w("HD_TBL const unsigned short hd_huff_canon_sym[257] = {")
+    for i in range(0, 257, 16):
+        w("  " + ", ".join("%d" % s for s in t["order"][i:i + 16]) + ",")
+    w("};")
+    for name, arr, n in (("hd_huff_first", t["first"], 32),
+                         ("hd_huff_base", t["base"], 32),
+                         ("hd_huff_count", t["count"], 32)):
+        vals = list(arr) + [0] * (n - len(arr))
+        w("HD_TBL const unsigned int %s[%d] = {" % (name, n))
+        w("  " + ", ".join("%du" % v for v in vals[:n]) + ",")
+        w("};")
+    w("HD_TBL const unsigned int hd_huff_depth_lo[30] = {")
+    w("  " + ", ".join("%du" % v for v in t["depth_lo"]) + ",")
+    w("};")
+    w("HD_TBL const unsigned short hd_huff_depth_base[30] = {")
+    w("  " + ", ".join("%d" % v for v in t["depth_base"]) + ",")
+    w("};")
+    w("HD_TBL const unsigned char hd_huff_depth_ids[256] = {")
+    for i in range(0, 256, 16):
+        w("  " + ", ".join("%d" % v for v in t["id_list"][i:i + 16]) + ",")
+    w("};")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = os.path.join(here, "..", "csrc", "hd_huff_tables.inc")
+    if len(sys.argv) > 1:
+        out = sys.argv[1]
+    t = build()
+    write_inc(t, out)
+    sym, dec = packed_ref_layout(t)
+    print("sym sha256", hashlib.sha256(sym).hexdigest())
+    print("fsm sha256", hashlib.sha256(dec).hexdigest())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the oracle, bit-exact.
+
+Encode: encoded offsets (== nghttp2_hd_huff_encode_count per string) and
+every encoded byte.  Decode: per-string status (length / -523 / -502), final
+decode context {fstate, flags}, and the whole zero-initialised output slot
+pool (decoded bytes plus the bytes a failing string leaves behind, exactly as
+lib/nghttp2_hd_huffman.c:122-133 writes them).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.golden import make_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def to_dev(a, dev, dtype=None):
+    import torch
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).to(dev)
+
+
+def pad16(pool, used):
+    out = np.zeros(int(used) + (-int(used)) % 16 + 16, dtype=np.uint8)
+    out[:int(used)] = pool[:int(used)]
+    return out
+
+
+def gpu_encode(codec, dev, pool, off):
+    src = to_dev(pad16(pool, off[-1]), dev)
+    enc, enc_off = codec.encode(src, to_dev(off, dev), raw_bytes=int(off[-1]))
+    eo = enc_off.cpu().numpy().view(np.uint32).copy()
+    return enc.cpu().numpy()[:int(eo[-1])], eo
+
+
+def gpu_decode(codec, dev, enc, eoff):
+    import torch
+    src = to_dev(pad16(enc, eoff[-1]), dev)
+    so = to_dev(eoff, dev)
+    dst_off = codec.decode_slots(so)
+    cap = int(dst_off[-1].item())
+    dst = torch.zeros(cap + 16, dtype=torch.uint8, device=dev)
+    dst, dst_off, st, fs, fl = codec.decode(src, so, dst_off=dst_off, dst=dst, want_ctx=True)
+    torch.cuda.synchronize()
+    return (dst.cpu().numpy()[:cap], dst_off.cpu().numpy().view(np.uint32),
+            st.cpu().numpy(), fs.cpu().numpy().view(np.uint16), fl.cpu().numpy())
+
+
+def check_decode(codec, dev, enc, eoff, tag):
+    d, do, st, fs, fl = gpu_decode(codec, dev, enc, eoff)
+    rd, rdo, rst, rfs, rfl = O.decode_batch(enc, eoff)
+    assert np.array_equal(do, rdo), tag + ": slots"
+    bad = np.nonzero(st != rst)[0]
+    assert bad.size == 0, "%s: status differs at %s (gpu %s, ref %s)" % (
+        tag, bad[:5], st[bad[:5]], rst[bad[:5]])
+    assert np.array_equal(fs, rfs), tag + ": fstate"
+    assert np.array_equal(fl, rfl), tag + ": flags"
+    if not np.array_equal(d, rd[:len(d)]):
+        i = int(np.nonzero(d != rd[:len(d)])[0][0])
+        s = int(np.searchsorted(do, i, side="right") - 1)
+        raise AssertionError("%s: output differs at byte %d (string %d)" % (tag, i, s))
+    return st
+
+
+def check_roundtrip(codec, dev, pool, off, tag):
+    enc, eoff = gpu_encode(codec, dev, pool, off)
+    renc, reoff = O.encode_batch(pool, off)
+    assert np.array_equal(eoff, reoff), tag + ": encoded offsets"
+    if not np.array_equal(enc, renc):
+        i = int(np.nonzero(enc != renc)[0][0])
+        raise AssertionError("%s: encoded byte %d differs" % (tag, i))
+    st = check_decode(codec, dev, enc, eoff, tag)
+    assert np.array_equal(st, np.diff(off.astype(np.int64))), tag + ": round trip lengths"
+
+
+@pytest.mark.parametrize("name", make_golden.CASES)
+def test_golden(codec, dev, name):
+    g = make_golden.load(name)
+    if g["kind"] == "roundtrip":
+        enc, eoff = gpu_encode(codec, dev, g["raw"], g["raw_off"])
+        assert np.array_equal(eoff, g["enc_off"])
+        assert np.array_equal(enc, g["enc"][:int(eoff[-1])])
+    enc, eoff = g["enc"], g["enc_off"]
+    d, do, st, fs, fl = gpu_decode(codec, dev, enc, eoff)
+    assert np.array_equal(st, g["status"])
+    assert np.array_equal(fs, g["fstate"])
+    assert np.array_equal(fl, g["flags"])
+    assert hashlib.sha256(make_golden.decoded_bytes(d, do, st)).hexdigest() == g["dec_sha256"]
+
+
+def test_known_answers(codec, dev):
+    import json, os
+    ka = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    vecs = [v for v in ka["ref_unit_decode"] if v["final"]]
+    strs = [bytes.fromhex(v["src"]) for v in vecs]
+    strs += [bytes.fromhex(h) for _, h in ka["rfc7541"]]
+    lens = np.array([len(s) for s in strs], dtype=np.int64)
+    from nghttp2_amd import workloads as W
+    pool, off = W._pool_from_lengths(lens, np.frombuffer(b"".join(strs), np.uint8))
+    d, do, st, fs, fl = gpu_decode(codec, dev, pool, off)
+    for i, v in enumerate(vecs):
+        exp = v["rv"] if v["rv"] < 0 else len(bytes.fromhex(v.get("out", "")))
+        assert st[i] == exp, v
+        if "failure_state" in v:
+            assert (fs[i] == 0x100) == v["failure_state"], v
+    for j, (s, h) in enumerate(ka["rfc7541"]):
+        i = len(vecs) + j
+        assert st[i] == len(s)
+        assert bytes(d[do[i]:do[i] + len(s)]) == s.encode()
+    raw = [s.encode() for s, _ in ka["rfc7541"]]
+    lens = np.array([len(s) for s in raw], dtype=np.int64)
+    pool, off = W._pool_from_lengths(lens, np.frombuffer(b"".join(raw), np.uint8))
+    enc, eoff = gpu_encode(codec, dev, pool, off)
+    for j, (s, h) in enumerate(ka["rfc7541"]):
+        assert bytes(enc[eoff[j]:eoff[j + 1]]).hex() == h
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 4095, 4096, 4097, 20000])
+def test_batch_sizes(codec, dev, n):
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(n, seed=100 + n)
+    check_roundtrip(codec, dev, pool, off, "pseudo n=%d" % n)
+
+
+def test_all_byte_values(codec, dev):
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_all_bytes(30000, seed=5)
+    check_roundtrip(codec, dev, pool, off, "allbytes")
+
+
+def test_empty_and_ragged(codec, dev):
+    from nghttp2_amd import workloads as W
+    rng = np.random.default_rng(9)
+    lens = rng.choice([0, 0, 1, 2, 3, 15, 16, 17, 31, 33, 300], size=9000)
+    chars = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    pool, off = W._pool_from_lengths(lens, chars)
+    check_roundtrip(codec, dev, pool, off, "ragged")
+    lens = np.zeros(5000, dtype=np.int64)
+    pool, off = W._pool_from_lengths(lens, np.zeros(0, np.uint8))
+    check_roundtrip(codec, dev, pool, off, "all-empty")
+
+
+def test_max_length_strings(codec, dev):
+    # NGHTTP2_HD_MAX_NV (lib/nghttp2_hd.h:45) sized literals
+    from nghttp2_amd import workloads as W
+    rng = np.random.default_rng(12)
+    lens = np.array([65536, 1, 65536, 70000, 0, 65535], dtype=np.int64)
+    chars = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    pool, off = W._pool_from_lengths(lens, chars)
+    check_roundtrip(codec, dev, pool, off, "max-len")
+
+
+def test_adversarial_decode(codec, dev):
+    from nghttp2_amd import workloads as W
+    pool, off, cats = W.gen_adversarial(50000, seed=77)
+    st = check_decode(codec, dev, pool, off, "adversarial")
+    # every malformed category produces errors somewhere
+    for c in (1, 2, 4):
+        assert (st[cats == c] < 0).any()
+
+
+def test_random_garbage_decode(codec, dev):
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_all_bytes(40000, seed=21, lo=0, hi=48)
+    check_decode(codec, dev, pool, off, "garbage")
+
+
+def test_small_slots_buffer_error(codec, dev):
+    """Caller-provided slots smaller than the decoded length -> -502, no
+    write outside the slot."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(2000, seed=3)
+    enc, eoff = O.encode_batch(pool, off)
+    raw = np.diff(off.astype(np.int64))
+    cap = raw.copy()
+    cap[::3] -= 1
+    cap = np.maximum(cap, 0)
+    doff = np.zeros(len(off), dtype=np.uint32)
+    doff[1:] = np.cumsum(cap)
+    src = to_dev(pad16(enc, eoff[-1]), dev)
+    dst = torch.full((int(doff[-1]) + 16,), 0xAB, dtype=torch.uint8, device=dev)
+    _, _, st = codec.decode(src, to_dev(eoff, dev), dst_off=to_dev(doff, dev), dst=dst)
+    st = st.cpu().numpy()
+    exp = np.where(cap < raw, O.NGHTTP2_ERR_BUFFER_ERROR, raw)
+    assert np.array_equal(st, exp)
+    d = dst.cpu().numpy()
+    assert (d[int(doff[-1]):] == 0xAB).all()
+    for i in range(0, 2000, 7):
+        k = min(cap[i], raw[i])
+        assert bytes(d[doff[i]:doff[i] + k]) == bytes(pool[off[i]:off[i] + k])
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_full_size_config_roundtrip(codec, dev, cfg):
+    """BASELINE.json configs 2/3 at full size (1M strings): bit-exact vs the
+    oracle (multi-threaded) and decode(encode(x)) == x."""
+    from nghttp2_amd import workloads as W
+    n = 1 << 20
+    pool, off = W.gen_pseudo_headers(n) if cfg == 2 else W.gen_mixed_values(n)
+    enc, eoff = gpu_encode(codec, dev, pool, off)
+    renc, reoff = O.encode_batch(pool, off, nthreads=16)
+    assert np.array_equal(eoff, reoff)
+    assert hashlib.sha256(enc.tobytes()).digest() == hashlib.sha256(renc.tobytes()).digest()
+    d, do, st, fs, fl = gpu_decode(codec, dev, enc, eoff)
+    raw = np.diff(off.astype(np.int64))
+    assert np.array_equal(st, raw)
+    assert (fl & 1).all()
+    # checksum of checksums: every string's bytes land in its slot
+    idx = np.repeat(do[:-1].astype(np.int64), raw) + (np.arange(int(raw.sum()))
+                                                      - np.repeat(off[:-1].astype(np.int64), raw))
+    assert np.array_equal(d[idx], pool[:int(off[-1])])
