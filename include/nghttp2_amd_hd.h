@@ -20,8 +20,8 @@
  *     (lib/nghttp2_hd.h:394-440) -- see nghttp2_amd_hd_huffman_compat.h.
  *
  * Pool requirements (device API): pool base pointers 16-byte aligned; the
- * source pool readable up to align_up(off[N], 16) bytes (kernels load
- * aligned 16-byte words).  Offsets are uint32, so one batch's pool is
+ * source pool readable up to align_up(off[N], 16) + 16 bytes (kernels load
+ * aligned 16-byte words and unaligned 4-byte windows).  Offsets are uint32, so one batch's pool is
  * < 4 GiB; shard larger sets (multi-GPU).
  *
  * Error convention: 0 on success or a negative nghttp2_error code
@@ -70,6 +70,11 @@ int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out);
  * every symbol is at most 30 bits (RFC 7541 App. B), plus one padding byte
  * per string, rounded up to 16. */
 size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n);
+
+/* Size of the decode output pool nghttp2_amd_hd_huff_decode_batch_auto needs
+ * for an encoded pool of `enc_bytes` bytes in `n` strings:
+ * floor(8 * enc_bytes / 5) + n, rounded up. */
+size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n);
 
 /* Bytes of device workspace nghttp2_amd_hd_huff_encode_batch and
  * nghttp2_amd_hd_huff_decode_slots need for `n` strings. */
@@ -149,6 +154,37 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                                      const uint32_t *dst_off, int32_t *status,
                                      uint16_t *fstate, uint8_t *flags,
                                      void *stream);
+
+/*
+ * Same as nghttp2_amd_hd_huff_decode_batch, with the engine assigning the
+ * output slots in the same launch: dst_off[i] = floor(8*(src_off[i] -
+ * src_off[0])/5) + i (OUT, n+1 entries).  Each slot holds at least
+ * floor(8*E_i/5)+1 bytes -- the reference's allocation -- so no string can
+ * overflow; dst_cap must be >= nghttp2_amd_hd_huff_decode_bound(E_total, n)
+ * (strings whose slot would end past dst_cap get -502 and write nothing).
+ */
+int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
+                                          uint32_t n, uint8_t *dst, size_t dst_cap,
+                                          uint32_t *dst_off, int32_t *status,
+                                          uint16_t *fstate, uint8_t *flags, void *stream);
+
+/*
+ * The reference's nibble-stepped FSM itself (lib/nghttp2_hd_huffman.c:111-143
+ * over huff_decode_table, :122-133), batched: an exact cross-check of the
+ * canonical decoder and the path for chunked (streaming) input.  Each string
+ * i starts from the decode context {init_fstate[i], init_flags[i]} (both
+ * NULL: nghttp2_hd_huff_decode_context_init, :106-109), the final context is
+ * written to fstate/flags (optional), and `final` is the reference's fin
+ * flag: when nonzero a non-accepting end state gives -523, else status is
+ * the number of bytes written (the reference returns srclen then; the
+ * caller checks fstate == 0x100 for failure_state, :145-147).
+ */
+int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src_off,
+                                         uint32_t n, uint8_t *dst, const uint32_t *dst_off,
+                                         int32_t *status, uint16_t *fstate, uint8_t *flags,
+                                         const uint16_t *init_fstate,
+                                         const uint8_t *init_flags, int final,
+                                         void *stream);
 
 #ifdef __cplusplus
 }

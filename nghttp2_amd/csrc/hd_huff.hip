@@ -3,24 +3,25 @@
 // Replaces the reference's scalar loops in lib/nghttp2_hd_huffman.c
 // (encode_count :34-43, encode :45-104, decode :111-143) for batches of
 // independent header strings laid out SoA in HBM (see
-// include/nghttp2_amd_hd.h and DESIGN.md).
+// include/nghttp2_amd_hd.h and DESIGN.md).  Integer/table work only (no
+// MFMA): HBM-bound streaming with the code tables staged in LDS.
 //
-// Kernel set (all integer/table work, no MFMA):
-//   k_enc_count   per-string encoded length (sum of code lengths) + per-tile
-//                 sums for the offset scan
+// Kernels
+//   k_enc_count   one string per lane: E = ceil(sum of code lengths / 8),
+//                 plus the per-256-string tile sum for the offset scan
 //   k_scan_tiles  exclusive scan of the tile sums (one workgroup)
-//   k_scan_apply  in-tile exclusive scan -> offsets (decode slots)
-//   k_encode      in-tile scan -> encoded offsets, then MSB-first bit packing
-//                 with EOS-prefix padding (lib/nghttp2_hd_huffman.c:95-101)
-//   k_decode      nibble-stepped FSM (lib/nghttp2_hd_huffman.c:122-133) over
-//                 the 257x16 transition table staged in LDS
-//
-// Work layout: a workgroup (256 lanes) owns a tile of TILE consecutive
-// strings; lane t owns strings [tile*TILE + t*SPL, +SPL), whose input bytes
-// and output bytes are each one contiguous stream, so every lane reads its
-// input with aligned 16-byte loads and writes whole aligned 32-bit words
-// except at its two stream ends.  Tables are staged in LDS once per
-// workgroup.
+//   k_encode      tile scan -> encoded offsets, then MSB-first bit packing
+//                 into aligned 32-bit words with EOS-prefix (all ones)
+//                 padding (lib/nghttp2_hd_huffman.c:57-101)
+//   k_decode      persistent workgroups, one string per lane: canonical
+//                 decode with a 12-bit / 2-symbol lookup table in LDS and an
+//                 unrolled compare ladder for codes > 12 bits; the final
+//                 {fstate, flags} of the reference's nibble FSM
+//                 (lib/nghttp2_hd_huffman.c:122-136) is rebuilt exactly from
+//                 the undecoded tail bits (DESIGN.md "decode state")
+//   k_decode_fsm  the reference's nibble FSM itself (257x16 table in LDS),
+//                 kept as the exact cross-check path and for chunked calls
+//   k_slot_len / k_scan_apply   tight decode slots (floor(8E/5)+1 each)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -40,19 +41,18 @@ namespace host {
 #undef HD_TBL
 }  // namespace host
 
-#define WG 256
-#define SPL 16
-#define TILE (WG * SPL)
+#define WG 256          // lanes per workgroup; also strings per scan tile
 #define SCAN_WG 1024
+#define DEC_WG_PER_CU 8 // persistent decode grid: 256 CUs x 8 workgroups
+#define NUM_CU 256
 
 #define HUFF_ACCEPTED 0x01u
 #define HUFF_SYM 0x02u
+#define FAIL_STATE 0x100u
 
 // ---------------------------------------------------------------------------
-// small device helpers
+// device helpers
 // ---------------------------------------------------------------------------
-
-// Inclusive scan across the 64 lanes of a wave.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -63,8 +63,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// Exclusive scan across a workgroup of NT threads; returns the exclusive
-// prefix, writes the workgroup total to *total.  `sm` needs NT/64 words.
+// Exclusive scan across a workgroup of NT threads (NT/64 words of `sm`).
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sm,
                                                     uint32_t *total) {
@@ -85,48 +84,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sm,
   return wpre + inc - v;
 }
 
-// Byte stream reader over [p, end) of the pool with aligned 16-byte loads.
-// The pool is readable up to align_up(end, 16) (API contract).
-struct ByteIn {
-  const uint8_t *base;
-  uint32_t pos;     // absolute byte index of the next byte
-  uint32_t chunk;   // absolute index of the loaded chunk (multiple of 16)
-  uint4 v;
-  __device__ __forceinline__ void init(const uint8_t *b, uint32_t p) {
-    base = b;
-    pos = p;
-    chunk = 0xFFFFFFFFu;
-  }
-  __device__ __forceinline__ uint32_t get() {
-    uint32_t c = pos & ~15u;
-    if (c != chunk) {
-      chunk = c;
-      v = *reinterpret_cast<const uint4 *>(base + c);
-    }
-    uint32_t k = pos & 15u;
-    uint32_t w = (k < 8) ? ((k < 4) ? v.x : v.y) : ((k < 12) ? v.z : v.w);
-    ++pos;
-    return (w >> ((k & 3u) * 8u)) & 0xFFu;
-  }
-};
-
-// Byte stream writer: packs bytes into aligned 32-bit words; the (up to)
-// partial words at the two ends of a stream go out as single bytes, so two
-// lanes whose streams share a word never overwrite each other's bytes.
+// Byte-stream writer for decode output: packs bytes into aligned 32-bit
+// words; partial words at the two ends go out byte by byte, so neighbouring
+// strings never overwrite each other's bytes.
 struct ByteOut {
-  uint8_t *p;   // address of the first pending byte
-  uint32_t w;   // pending bytes, little-endian from p
-  uint32_t k;   // pending byte count (0..3)
-  __device__ __forceinline__ void init(uint8_t *q) {
-    p = q;
-    w = 0;
-    k = 0;
-  }
+  uint8_t *p;
+  uint32_t w, k;
+  __device__ __forceinline__ void init(uint8_t *q) { p = q; w = 0; k = 0; }
   __device__ __forceinline__ void flush() {
     for (uint32_t i = 0; i < k; ++i) p[i] = (uint8_t)(w >> (8 * i));
-    p += k;
-    w = 0;
-    k = 0;
+    p += k; w = 0; k = 0;
   }
   __device__ __forceinline__ void put(uint32_t b) {
     w |= b << (8 * k);
@@ -134,9 +101,7 @@ struct ByteOut {
     if ((((uintptr_t)p + k) & 3u) == 0) {
       if (k == 4) {
         *reinterpret_cast<uint32_t *>(p) = w;
-        p += 4;
-        w = 0;
-        k = 0;
+        p += 4; w = 0; k = 0;
       } else {
         flush();
       }
@@ -144,219 +109,389 @@ struct ByteOut {
   }
 };
 
+// Word writer for encode output: the stream [o, o+E) receives big-endian
+// 32-bit groups; with phase = o & 3 fixed, each group completes one aligned
+// word (funnel shift with the pending bytes).  The head word that also holds
+// the previous string's bytes, and the tail, are written byte by byte.
+struct WordOut {
+  uint8_t *base;
+  uint32_t q, o, phase, pend;
+  __device__ __forceinline__ void init(uint8_t *b, uint32_t start) {
+    base = b; q = start; o = start; phase = start & 3u; pend = 0;
+  }
+  __device__ __forceinline__ void put32(uint32_t be) {
+    const uint32_t le = __builtin_bswap32(be);
+    if (phase == 0) {
+      *reinterpret_cast<uint32_t *>(base + q) = le;
+    } else {
+      const uint32_t word = pend | (le << (8 * phase));
+      const uint32_t wa = q & ~3u;
+      if (wa < o) {
+        for (uint32_t k = phase; k < 4; ++k) base[wa + k] = (uint8_t)(word >> (8 * k));
+      } else {
+        *reinterpret_cast<uint32_t *>(base + wa) = word;
+      }
+      pend = le >> (8 * (4 - phase));
+    }
+    q += 4;
+  }
+  // append the top `nbytes` (0..4) bytes of `be`, then drain everything
+  __device__ __forceinline__ void finish(uint32_t be, uint32_t nbytes) {
+    if (q > o) {
+      const uint32_t wa = q & ~3u;
+      for (uint32_t k = 0; k < phase; ++k) base[wa + k] = (uint8_t)(pend >> (8 * k));
+    }
+    for (uint32_t k = 0; k < nbytes; ++k) base[q + k] = (uint8_t)(be >> (24 - 8 * k));
+  }
+};
+
+// 4 bytes at an arbitrary pool position, big-endian (first byte in bits
+// 31..24); bytes at or past `end` read as zero.  Reads stay within
+// align_up(end, 16) + 4 (pool padding contract).
+__device__ __forceinline__ uint32_t load_be32(const uint8_t *base, uint32_t pos, uint32_t end) {
+  const uint32_t a = pos & ~3u;
+  const uint32_t w0 = *reinterpret_cast<const uint32_t *>(base + a);
+  const uint32_t w1 = *reinterpret_cast<const uint32_t *>(base + a + 4);
+  uint32_t x = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
+  const uint32_t v = end - pos;
+  if (v < 4) x &= ~(0xFFFFFFFFu >> (8 * v));
+  return x;
+}
+
 // ---------------------------------------------------------------------------
-// encode: lengths + tile sums   (lib/nghttp2_hd_huffman.c:34-43)
+// encode, pass 1: per-string encoded length  (lib/nghttp2_hd_huffman.c:34-43)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
                                                   const uint32_t *__restrict__ off,
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
                                                   uint32_t *__restrict__ tile_sums) {
-  __shared__ uint32_t lenT[256];
+  __shared__ uint8_t lenT[256];
   __shared__ uint32_t red[WG / 64];
   lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
   __syncthreads();
-  const uint32_t s0 = blockIdx.x * TILE + threadIdx.x * SPL;
-  uint32_t lane_sum = 0;
-  if (s0 < n) {
-    const uint32_t s1 = min(s0 + SPL, n);
-    ByteIn in;
-    uint32_t a = off[s0];
-    in.init(src, a);
-    for (uint32_t s = s0; s < s1; ++s) {
-      const uint32_t b = off[s + 1];
-      uint32_t bits = 0;
-      for (uint32_t p = a; p < b; ++p) bits += lenT[in.get()];
-      const uint32_t e = (bits + 7u) >> 3;
-      if (out_len) out_len[s] = e;
-      lane_sum += e;
-      a = b;
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  uint32_t e = 0;
+  if (s < n) {
+    const uint32_t a = off[s], b = off[s + 1];
+    uint32_t bits = 0;
+    for (uint32_t c = a & ~15u; c < b; c += 16) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(src + c);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t p = c + j;
+        const uint32_t L = lenT[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+        bits += (p >= a && p < b) ? L : 0u;
+      }
     }
+    e = (bits + 7u) >> 3;
+    if (out_len) out_len[s] = e;
   }
   if (tile_sums) {
     uint32_t tot;
-    block_excl_scan<WG>(lane_sum, red, &tot);
+    block_excl_scan<WG>(e, red, &tot);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
   }
 }
 
 // decode slots: cap_i = floor(8 E_i / 5) + 1 (lib/nghttp2_hd_huffman.h:76-78)
-__global__ __launch_bounds__(WG) void k_slot_len(const uint32_t *__restrict__ off,
-                                                 uint32_t n,
+__global__ __launch_bounds__(WG) void k_slot_len(const uint32_t *__restrict__ off, uint32_t n,
                                                  uint32_t *__restrict__ out_len,
                                                  uint32_t *__restrict__ tile_sums) {
   __shared__ uint32_t red[WG / 64];
-  const uint32_t s0 = blockIdx.x * TILE + threadIdx.x * SPL;
-  uint32_t lane_sum = 0;
-  for (uint32_t j = 0; j < SPL; ++j) {
-    const uint32_t s = s0 + j;
-    if (s < n) {
-      const uint32_t e = off[s + 1] - off[s];
-      const uint32_t c = (uint32_t)(((uint64_t)e * 8u) / 5u) + 1u;
-      out_len[s] = c;
-      lane_sum += c;
-    }
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  uint32_t c = 0;
+  if (s < n) {
+    const uint32_t e = off[s + 1] - off[s];
+    c = (uint32_t)(((uint64_t)e * 8u) / 5u) + 1u;
+    out_len[s] = c;
   }
   uint32_t tot;
-  block_excl_scan<WG>(lane_sum, red, &tot);
+  block_excl_scan<WG>(c, red, &tot);
   if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
 }
 
-// Exclusive scan of ntiles tile sums in place; writes the grand total to
-// *grand (== offsets[n]).
+// Exclusive scan of the tile sums in place (4 per thread per round); writes
+// the grand total to *grand (== offsets[n]).
 __global__ __launch_bounds__(SCAN_WG) void k_scan_tiles(uint32_t *__restrict__ tile_sums,
                                                         uint32_t ntiles,
                                                         uint32_t *__restrict__ grand) {
   __shared__ uint32_t sm[SCAN_WG / 64];
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < ntiles; base += SCAN_WG) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t v = (i < ntiles) ? tile_sums[i] : 0u;
+  for (uint32_t base = 0; base < ntiles; base += 4 * SCAN_WG) {
+    const uint32_t i0 = base + 4 * threadIdx.x;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = (i0 + j < ntiles) ? tile_sums[i0 + j] : 0u;
+      sum += v[j];
+    }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<SCAN_WG>(v, sm, &tot);
-    if (i < ntiles) tile_sums[i] = carry + ex;
+    uint32_t run = carry + block_excl_scan<SCAN_WG>(sum, sm, &tot);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j < ntiles) tile_sums[i0 + j] = run;
+      run += v[j];
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) *grand = carry;
 }
 
-// In-place: offs[i] holds a length on entry, the exclusive prefix on exit.
-__device__ __forceinline__ uint32_t tile_offsets(uint32_t *offs, uint32_t n,
-                                                 const uint32_t *tile_prefix,
-                                                 uint32_t *red, uint32_t loc[SPL]) {
-  const uint32_t s0 = blockIdx.x * TILE + threadIdx.x * SPL;
-  uint32_t lane_sum = 0;
-#pragma unroll
-  for (int j = 0; j < SPL; ++j) {
-    const uint32_t s = s0 + j;
-    loc[j] = (s < n) ? offs[s] : 0u;
-    lane_sum += loc[j];
-  }
-  uint32_t tot;
-  uint32_t run = tile_prefix[blockIdx.x] + block_excl_scan<WG>(lane_sum, red, &tot);
-#pragma unroll
-  for (int j = 0; j < SPL; ++j) {
-    const uint32_t s = s0 + j;
-    const uint32_t len = loc[j];
-    loc[j] = run;
-    if (s < n) offs[s] = run;
-    run += len;
-  }
-  return run;  // end offset of the lane's last string
-}
-
+// in-place: offs[s] holds a length on entry, the exclusive prefix on exit
 __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, uint32_t n,
                                                    const uint32_t *__restrict__ tile_prefix) {
   __shared__ uint32_t red[WG / 64];
-  uint32_t loc[SPL];
-  tile_offsets(offs, n, tile_prefix, red, loc);
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  const uint32_t len = (s < n) ? offs[s] : 0u;
+  uint32_t tot;
+  const uint32_t o = tile_prefix[blockIdx.x] + block_excl_scan<WG>(len, red, &tot);
+  if (s < n) offs[s] = o;
 }
 
 // ---------------------------------------------------------------------------
-// encode: bit packing    (lib/nghttp2_hd_huffman.c:45-104)
+// encode, pass 2: bit packing   (lib/nghttp2_hd_huffman.c:45-104)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
-                                               const uint32_t *__restrict__ off,
-                                               uint32_t n, uint8_t *__restrict__ dst,
-                                               uint64_t dst_cap,
+                                               const uint32_t *__restrict__ off, uint32_t n,
+                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
                                                const uint32_t *__restrict__ tile_prefix) {
   __shared__ uint2 codeT[256];
   __shared__ uint32_t red[WG / 64];
   codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x],
                                   dev::hd_huff_enc_len[threadIdx.x]);
-  uint32_t loc[SPL];
-  const uint32_t end_out = tile_offsets(dst_off, n, tile_prefix, red, loc);
-  __syncthreads();
-  const uint32_t s0 = blockIdx.x * TILE + threadIdx.x * SPL;
-  if (s0 >= n) return;
-  if ((uint64_t)end_out > dst_cap) return;  // never write past the pool
-  const uint32_t s1 = min(s0 + SPL, n);
-  ByteIn in;
-  uint32_t a = off[s0];
-  in.init(src, a);
-  ByteOut out;
-  out.init(dst + loc[0]);
-  for (uint32_t s = s0; s < s1; ++s) {
-    const uint32_t b = off[s + 1];
-    uint64_t acc = 0;  // MSB-aligned pending bits
-    uint32_t nb = 0;
-    for (uint32_t p = a; p < b; ++p) {
-      const uint2 e = codeT[in.get()];
-      acc |= (uint64_t)e.x << (32 - nb);
-      nb += e.y;
-      while (nb >= 8) {
-        out.put((uint32_t)(acc >> 56));
-        acc <<= 8;
-        nb -= 8;
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  const uint32_t E = (s < n) ? dst_off[s] : 0u;
+  uint32_t tot;
+  const uint32_t o = tile_prefix[blockIdx.x] + block_excl_scan<WG>(E, red, &tot);
+  if (s >= n) return;
+  dst_off[s] = o;
+  if ((uint64_t)o + E > dst_cap) return;  // never write past the pool
+  const uint32_t a = off[s], b = off[s + 1];
+  uint64_t acc = 0;  // MSB-aligned pending bits, nb < 32 between bytes
+  uint32_t nb = 0;
+  WordOut out;
+  out.init(dst, o);
+  for (uint32_t c = a & ~15u; c < b; c += 16) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(src + c);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t p = c + j;
+      if (p >= a && p < b) {
+        const uint2 e = codeT[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+        acc |= (uint64_t)e.x << (32 - nb);
+        nb += e.y;
+        if (nb >= 32) {
+          out.put32((uint32_t)(acc >> 32));
+          acc <<= 32;
+          nb -= 32;
+        }
       }
     }
-    if (nb) {  // pad with the EOS prefix (all ones)
-      out.put((uint32_t)(acc >> 56) | ((1u << (8 - nb)) - 1u));
-    }
-    a = b;
   }
-  out.flush();
+  // pad the last partial byte with the EOS prefix (all ones), :95-101
+  const uint32_t pad = (8u - (nb & 7u)) & 7u;
+  acc |= (~0ull >> nb) & ~(~0ull >> (nb + pad));
+  nb += pad;
+  out.finish((uint32_t)(acc >> 32), nb >> 3);
 }
 
 // ---------------------------------------------------------------------------
-// decode: nibble FSM    (lib/nghttp2_hd_huffman.c:111-143)
+// decode: canonical multi-symbol decoder
 // ---------------------------------------------------------------------------
+struct DecTables {
+  uint32_t lut[1 << HD_HUFF_LUT_BITS];
+  uint16_t canon[260];
+  uint32_t depth_lo[30];
+  uint16_t depth_base[30];
+  uint8_t depth_ids[256];
+};
+
+__device__ __forceinline__ void stage_dec_tables(DecTables &T) {
+  for (uint32_t i = threadIdx.x; i < (1u << HD_HUFF_LUT_BITS); i += WG) T.lut[i] = dev::hd_huff_lut[i];
+  for (uint32_t i = threadIdx.x; i < 257; i += WG) T.canon[i] = dev::hd_huff_canon_sym[i];
+  if (threadIdx.x < 30) {
+    T.depth_lo[threadIdx.x] = dev::hd_huff_depth_lo[threadIdx.x];
+    T.depth_base[threadIdx.x] = dev::hd_huff_depth_base[threadIdx.x];
+  }
+  T.depth_ids[threadIdx.x] = dev::hd_huff_depth_ids[threadIdx.x];
+  __syncthreads();
+}
+
+// Decode one string [a, b) into out.  Returns status; *fs / *fl receive the
+// final reference decode context (lib/nghttp2_hd_huffman.h:56-60).
+template <bool CHECK>
+__device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t *__restrict__ src,
+                                              uint32_t a, uint32_t b, uint8_t *__restrict__ dst,
+                                              uint32_t cap, uint32_t *fs, uint32_t *fl) {
+  ByteOut out;
+  out.init(dst);
+  uint64_t bb = 0;   // MSB-aligned bit buffer
+  uint32_t nb = 0;   // valid bits in bb
+  uint32_t pos = a;  // next byte to load
+  uint32_t rem = 8u * (b - a);  // bits of the string not yet decoded
+  uint32_t nsym = 0;
+  bool failed = false, ovf = false;
+  while (rem) {
+    if (nb <= 32 && pos < b) {
+      const uint32_t x = load_be32(src, pos, b);
+      const uint32_t v = min(4u, b - pos);
+      bb |= (uint64_t)x << (32 - nb);
+      nb += 8 * v;
+      pos += v;
+    }
+    const uint32_t e = T.lut[(uint32_t)(bb >> (64 - HD_HUFF_LUT_BITS))];
+    uint32_t L1 = (e >> 16) & 15u;
+    uint32_t sym;
+    if (L1 == 0) {
+      // code longer than the lookup: canonical length by left-justified limits
+      const uint32_t win = (uint32_t)(bb >> 32);
+      uint32_t first = 0, base = 0;
+#define HD_LONG_STEP(LEN, LIM, FIRST, BASE) \
+      if (L1 == 0 && (uint64_t)win < (LIM)) { L1 = (LEN); first = (FIRST); base = (BASE); }
+      HD_HUFF_LONG_CODES(HD_LONG_STEP)
+#undef HD_LONG_STEP
+      if (L1 > rem) break;
+      sym = T.canon[base + ((win >> (32 - L1)) - first)];
+      if (sym == 256) {  // EOS decoded: the FSM's sticky failure state
+        failed = true;
+        break;
+      }
+    } else {
+      if (L1 > rem) break;
+      sym = e & 0xFFu;
+    }
+    if (!CHECK || nsym < cap) out.put(sym); else ovf = true;
+    ++nsym;
+    bb <<= L1;
+    nb -= L1;
+    rem -= L1;
+    const uint32_t L2 = (e >> 20) & 15u;
+    if (L2 && L2 <= rem) {
+      if (!CHECK || nsym < cap) out.put((e >> 8) & 0xFFu); else ovf = true;
+      ++nsym;
+      bb <<= L2;
+      nb -= L2;
+      rem -= L2;
+    }
+  }
+  out.flush();
+  if (failed) {
+    *fs = FAIL_STATE;
+    *fl = 0;
+    return CHECK && ovf ? NGHTTP2_AMD_ERR_BUFFER_ERROR : NGHTTP2_AMD_ERR_HEADER_COMP;
+  }
+  // tail = the last `rem` (< 30) bits: a proper prefix of a code, i.e. an
+  // internal node of the code tree -> the FSM state it leaves behind.
+  const uint32_t t = rem;
+  const uint32_t v = t ? (uint32_t)(bb >> (64 - t)) : 0u;
+  const bool accept = (t <= 7) && (v == (1u << t) - 1u);
+  *fs = t ? T.depth_ids[T.depth_base[t] + (v - T.depth_lo[t])] : 0u;
+  *fl = (accept ? HUFF_ACCEPTED : 0u) | ((t < 4 && nsym) ? HUFF_SYM : 0u);
+  if (CHECK && ovf) return NGHTTP2_AMD_ERR_BUFFER_ERROR;
+  return accept ? (int32_t)nsym : NGHTTP2_AMD_ERR_HEADER_COMP;
+}
+
+// AUTO: the engine assigns slots dst_off[s] = floor(8 (off[s]-off[0]) / 5)
+// + s (>= the reference's floor(8E/5)+1 per string, so no check needed) and
+// writes them out; else caller slots, capacity-checked.
+template <bool AUTO>
 __global__ __launch_bounds__(WG) void k_decode(const uint8_t *__restrict__ src,
-                                               const uint32_t *__restrict__ off,
-                                               uint32_t n, uint8_t *__restrict__ dst,
-                                               const uint32_t *__restrict__ dst_off,
+                                               const uint32_t *__restrict__ off, uint32_t n,
+                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                               uint32_t *__restrict__ dst_off,
                                                int32_t *__restrict__ status,
                                                uint16_t *__restrict__ fstate_out,
                                                uint8_t *__restrict__ flags_out) {
+  __shared__ DecTables T;
+  stage_dec_tables(T);
+  const uint32_t off0 = off[0];
+  for (uint32_t s = blockIdx.x * WG + threadIdx.x; s < n; s += gridDim.x * WG) {
+    const uint32_t a = off[s], b = off[s + 1];
+    uint32_t o, cap;
+    if (AUTO) {
+      const uint64_t o64 = ((uint64_t)(a - off0) * 8u) / 5u + s;
+      const uint64_t e64 = ((uint64_t)(b - off0) * 8u) / 5u + s + 1;
+      o = (uint32_t)o64;
+      cap = (uint32_t)(e64 - o64);
+      dst_off[s] = o;
+      if (s == n - 1) dst_off[n] = (uint32_t)e64;
+      if (e64 > dst_cap) {
+        status[s] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+        continue;
+      }
+    } else {
+      o = dst_off[s];
+      cap = dst_off[s + 1] - o;
+    }
+    uint32_t fs, fl;
+    const int32_t st = decode_one<!AUTO>(T, src, a, b, dst + o, cap, &fs, &fl);
+    status[s] = st;
+    if (fstate_out) fstate_out[s] = (uint16_t)fs;
+    if (flags_out) flags_out[s] = (uint8_t)fl;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// decode: the reference's nibble FSM   (lib/nghttp2_hd_huffman.c:111-143)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ src,
+                                                   const uint32_t *__restrict__ off, uint32_t n,
+                                                   uint8_t *__restrict__ dst,
+                                                   const uint32_t *__restrict__ dst_off,
+                                                   int32_t *__restrict__ status,
+                                                   uint16_t *__restrict__ fstate_out,
+                                                   uint8_t *__restrict__ flags_out,
+                                                   const uint16_t *__restrict__ init_state,
+                                                   const uint8_t *__restrict__ init_flags,
+                                                   int final) {
   __shared__ uint32_t fsm[257 * 16];
   for (uint32_t i = threadIdx.x; i < 257 * 16; i += WG) fsm[i] = dev::hd_huff_fsm[i];
   __syncthreads();
-  const uint32_t s0 = blockIdx.x * TILE + threadIdx.x * SPL;
-  if (s0 >= n) return;
-  const uint32_t s1 = min(s0 + SPL, n);
-  ByteIn in;
-  uint32_t a = off[s0];
-  in.init(src, a);
-  for (uint32_t s = s0; s < s1; ++s) {
-    const uint32_t b = off[s + 1];
+  for (uint32_t s = blockIdx.x * WG + threadIdx.x; s < n; s += gridDim.x * WG) {
+    const uint32_t a = off[s], b = off[s + 1];
     const uint32_t o0 = dst_off[s];
     const uint32_t cap = dst_off[s + 1] - o0;
     ByteOut out;
     out.init(dst + o0);
-    uint32_t t = (HUFF_ACCEPTED << 16);  // {fstate 0, flags ACCEPTED}
+    uint32_t t = init_state ? (uint32_t)init_state[s] | ((uint32_t)init_flags[s] << 16)
+                            : (HUFF_ACCEPTED << 16);
     uint32_t w = 0;
     bool overflow = false;
-    for (uint32_t p = a; p < b; ++p) {
-      const uint32_t c = in.get();
-      t = fsm[(t & 0x1FFu) * 16u + (c >> 4)];
-      if (t & (HUFF_SYM << 16)) {
-        if (w < cap) out.put(t >> 24); else overflow = true;
-        ++w;
-      }
-      t = fsm[(t & 0x1FFu) * 16u + (c & 15u)];
-      if (t & (HUFF_SYM << 16)) {
-        if (w < cap) out.put(t >> 24); else overflow = true;
-        ++w;
+    for (uint32_t p = a; p < b; p += 4) {
+      const uint32_t x = load_be32(src, p, b);
+      const uint32_t nbytes = min(4u, b - p);
+      for (uint32_t k = 0; k < 2 * nbytes; ++k) {
+        t = fsm[(t & 0x1FFu) * 16u + ((x >> (28 - 4 * k)) & 15u)];
+        if (t & (HUFF_SYM << 16)) {
+          if (w < cap) out.put(t >> 24); else overflow = true;
+          ++w;
+        }
       }
     }
     out.flush();
     const uint32_t flags = (t >> 16) & 0xFFu;
     int32_t st;
     if (overflow) st = NGHTTP2_AMD_ERR_BUFFER_ERROR;
-    else if (!(flags & HUFF_ACCEPTED)) st = NGHTTP2_AMD_ERR_HEADER_COMP;
+    else if (final && !(flags & HUFF_ACCEPTED)) st = NGHTTP2_AMD_ERR_HEADER_COMP;
     else st = (int32_t)w;
     status[s] = st;
     if (fstate_out) fstate_out[s] = (uint16_t)(t & 0xFFFFu);
     if (flags_out) flags_out[s] = (uint8_t)flags;
-    a = b;
   }
 }
 
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-static inline uint32_t ntiles_for(uint32_t n) { return (n + TILE - 1) / TILE; }
+static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
+static inline uint32_t persistent_grid(uint32_t n) {
+  uint32_t g = ntiles_for(n);
+  return g < NUM_CU * DEC_WG_PER_CU ? g : NUM_CU * DEC_WG_PER_CU;
+}
 
 static int hip_rv(hipError_t e) {
   if (e == hipSuccess) return 0;
@@ -366,7 +501,7 @@ static int hip_rv(hipError_t e) {
 
 extern "C" {
 
-const char *nghttp2_amd_hd_version(void) { return "nghttp2_amd_hd 0.1.0 gfx950"; }
+const char *nghttp2_amd_hd_version(void) { return "nghttp2_amd_hd 0.2.0 gfx950"; }
 
 int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out) {
   if (sym_out) {
@@ -385,6 +520,11 @@ size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n) {
   return (size_t)((b + 15u) & ~(uint64_t)15u);
 }
 
+size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n) {
+  uint64_t b = (enc_bytes * 8u) / 5u + (uint64_t)n + 16u;
+  return (size_t)((b + 15u) & ~(uint64_t)15u);
+}
+
 size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n) {
   return ((size_t)ntiles_for(n) + 16u) * sizeof(uint32_t);
 }
@@ -393,9 +533,8 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
                                            uint32_t n, uint32_t *enc_len, void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, st, src, src_off, n,
-                     enc_len, (uint32_t *)nullptr);
+  hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
+                     src_off, n, enc_len, (uint32_t *)nullptr);
   return hip_rv(hipGetLastError());
 }
 
@@ -441,9 +580,37 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                                      void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid(n)), dim3(WG), 0,
+                     (hipStream_t)stream, src, src_off, n, dst, (uint64_t)0,
+                     (uint32_t *)dst_off, status, fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
+int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
+                                          uint32_t n, uint8_t *dst, size_t dst_cap,
+                                          uint32_t *dst_off, int32_t *status,
+                                          uint16_t *fstate, uint8_t *flags, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_decode, dim3(ntiles_for(n)), dim3(WG), 0, st, src, src_off, n, dst,
-                     dst_off, status, fstate, flags);
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid(n)), dim3(WG), 0, st, src, src_off,
+                     n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
+int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src_off,
+                                         uint32_t n, uint8_t *dst, const uint32_t *dst_off,
+                                         int32_t *status, uint16_t *fstate, uint8_t *flags,
+                                         const uint16_t *init_fstate,
+                                         const uint8_t *init_flags, int final,
+                                         void *stream) {
+  if (n == 0) return 0;
+  if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((init_fstate == nullptr) != (init_flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(k_decode_fsm, dim3(persistent_grid(n)), dim3(WG), 0, (hipStream_t)stream,
+                     src, src_off, n, dst, dst_off, status, fstate, flags, init_fstate,
+                     init_flags, final);
   return hip_rv(hipGetLastError());
 }
 

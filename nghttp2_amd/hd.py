@@ -57,6 +57,12 @@ def lib():
         L.nghttp2_amd_hd_huff_encode_count_batch.argtypes = [vp, vp, u32, vp, vp]
         L.nghttp2_amd_hd_huff_decode_slots.argtypes = [vp, u32, vp, vp, sz, vp]
         L.nghttp2_amd_hd_huff_decode_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.nghttp2_amd_hd_huff_decode_bound.restype = sz
+        L.nghttp2_amd_hd_huff_decode_bound.argtypes = [ctypes.c_uint64, u32]
+        L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, u32, vp, sz, vp, vp, vp,
+                                                            vp, vp]
+        L.nghttp2_amd_hd_huff_decode_fsm_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp,
+                                                           vp, vp, ctypes.c_int, vp]
         _lib = L
     return _lib
 
@@ -143,6 +149,51 @@ class HuffmanBatchCodec:
             _p(src_off), n, _p(dst_off), _p(ws), ws.numel(), _stream(stream))
         _check(rv, "decode_slots")
         return dst_off
+
+    def decode_bound(self, enc_bytes, n):
+        return self.L.nghttp2_amd_hd_huff_decode_bound(int(enc_bytes), int(n))
+
+    def decode_auto(self, src, src_off, enc_bytes=None, dst=None, dst_off=None, status=None,
+                    want_ctx=False, stream=None):
+        """Decode with engine-assigned slots (one launch).  Returns
+        (dst, dst_off, status[, fstate, flags])."""
+        torch = self.torch
+        n = src_off.numel() - 1
+        if enc_bytes is None:
+            enc_bytes = src.numel()
+        if dst is None:
+            dst = torch.empty(self.decode_bound(enc_bytes, n), dtype=torch.uint8,
+                              device=self.device)
+        if dst_off is None:
+            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+        if status is None:
+            status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        fstate = flags = None
+        if want_ctx:
+            fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
+            flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        rv = self.L.nghttp2_amd_hd_huff_decode_batch_auto(
+            _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(status),
+            _p(fstate), _p(flags), _stream(stream))
+        _check(rv, "decode_batch_auto")
+        if want_ctx:
+            return dst, dst_off, status[:n], fstate[:n], flags[:n]
+        return dst, dst_off, status[:n]
+
+    def decode_fsm(self, src, src_off, dst_off, dst, init_fstate=None, init_flags=None,
+                   final=True, stream=None):
+        """The reference nibble FSM, batched (streaming-capable).  Returns
+        (status, fstate, flags)."""
+        torch = self.torch
+        n = src_off.numel() - 1
+        status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
+        flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        rv = self.L.nghttp2_amd_hd_huff_decode_fsm_batch(
+            _p(src), _p(src_off), n, _p(dst), _p(dst_off), _p(status), _p(fstate),
+            _p(flags), _p(init_fstate), _p(init_flags), 1 if final else 0, _stream(stream))
+        _check(rv, "decode_fsm_batch")
+        return status[:n], fstate[:n], flags[:n]
 
     def decode(self, src, src_off, dst_off=None, dst=None, dst_cap=None, status=None,
                want_ctx=False, stream=None):

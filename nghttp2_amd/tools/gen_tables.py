@@ -51,6 +51,7 @@ RFC7541_LEN = [
 
 ACCEPTED = 0x01
 SYM = 0x02
+LUT_BITS = 12
 FAIL_STATE = 256
 EOS = 256
 
@@ -162,9 +163,40 @@ def build():
         depth_base[d] = len(id_list)
         id_list.extend(ids[(v, d)] for v in vs)
     assert len(id_list) == 256
+
+    # 12-bit multi-symbol lookup table for the canonical decoder: for every
+    # 12-bit window, the first code if it is <= 12 bits (sym1, L1) and, when
+    # the rest of the window holds another whole code, the second (sym2, L2).
+    # Entry: sym1 | sym2 << 8 | L1 << 16 | L2 << 20; L1 == 0 means the first
+    # code is longer than 12 bits (all such codes start with >= 10 ones).
+    lut = []
+    for w in range(1 << LUT_BITS):
+        def first_code(v, nbits):
+            for L in range(1, nbits + 1):
+                sym = leaf.get((v >> (nbits - L), L))
+                if sym is not None:
+                    return sym, L
+            return None, 0
+        s1, L1 = first_code(w, LUT_BITS)
+        e = 0
+        if s1 is not None:
+            assert s1 != EOS
+            r = LUT_BITS - L1
+            s2, L2 = first_code(w & ((1 << r) - 1), r) if r else (None, 0)
+            e = s1 | (L1 << 16)
+            if s2 is not None:
+                e |= (s2 << 8) | (L2 << 20)
+        lut.append(e)
+    # long codes: (L, left-justified exclusive limit as a 32-bit-window
+    # compare, first code, canonical index base) for every length > LUT_BITS
+    longc = []
+    for L in range(LUT_BITS + 1, maxlen + 1):
+        if count[L]:
+            lim = (first[L] + count[L]) << (32 - L)
+            longc.append((L, lim, first[L], base[L]))
     return dict(enc=enc, fsm=fsm, order=order, count=count, first=first,
                 base=base, depth_lo=depth_lo, depth_base=depth_base,
-                id_list=id_list)
+                id_list=id_list, lut=lut, longc=longc)
 
 
 def packed_ref_layout(t):
@@ -221,6 +253,18 @@ def write_inc(t, path):
     for i in range(0, 256, 16):
         w("  " + ", ".join("%d" % v for v in t["id_list"][i:i + 16]) + ",")
     w("};")
+    w("/* canonical decoder: %d-bit lookup, sym1 | sym2 << 8 | L1 << 16 | L2 << 20 */" % LUT_BITS)
+    w("#define HD_HUFF_LUT_BITS %d" % LUT_BITS)
+    w("HD_TBL const unsigned int hd_huff_lut[%d] = {" % (1 << LUT_BITS))
+    for i in range(0, 1 << LUT_BITS, 8):
+        w("  " + ", ".join("0x%08Xu" % e for e in t["lut"][i:i + 8]) + ",")
+    w("};")
+    w("/* codes longer than the lookup: X(len, limit32 (exclusive, left-justified),"
+      " first code, canonical base); limit of the last is 2^32 */")
+    w("#define HD_HUFF_LONG_CODES(X) \\")
+    for L, lim, fc, b in t["longc"]:
+        w("  X(%d, 0x%XULL, 0x%Xu, %du) \\" % (L, lim, fc, b))
+    w("")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 

@@ -215,3 +215,91 @@ def test_full_size_config_roundtrip(codec, dev, cfg):
     idx = np.repeat(do[:-1].astype(np.int64), raw) + (np.arange(int(raw.sum()))
                                                       - np.repeat(off[:-1].astype(np.int64), raw))
     assert np.array_equal(d[idx], pool[:int(off[-1])])
+
+
+def _variant_inputs():
+    from nghttp2_amd import workloads as W
+    pool, off, _ = W.gen_adversarial(20000, seed=31)
+    yield "adversarial", pool, off
+    p2, o2 = W.gen_all_bytes(20000, seed=32, lo=0, hi=40)
+    yield "garbage", p2, o2
+    p3, o3 = W.gen_mixed_values(3000, seed=33)
+    e3, eo3 = O.encode_batch(p3, o3)
+    yield "mixed", e3, eo3
+
+
+@pytest.mark.parametrize("variant", ["auto", "fsm"])
+def test_decode_variants_match_oracle(codec, dev, variant):
+    """decode_batch_auto (engine slots) and the batched reference FSM kernel
+    agree with the oracle on status, final context and every written byte."""
+    import torch
+    for tag, enc, eoff in _variant_inputs():
+        rd, rdo, rst, rfs, rfl = O.decode_batch(enc, eoff)
+        src = to_dev(pad16(enc, eoff[-1]), dev)
+        so = to_dev(eoff, dev)
+        n = len(eoff) - 1
+        if variant == "auto":
+            cap = codec.decode_bound(int(eoff[-1]), n)
+            dst = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            dst, do, st, fs, fl = codec.decode_auto(src, so, dst=dst, want_ctx=True)
+            do = do.cpu().numpy().view(np.uint32)
+            exp_do = (8 * (eoff.astype(np.int64) - int(eoff[0]))) // 5 + np.arange(n + 1)
+            assert np.array_equal(do, exp_do), tag
+        else:
+            do_t = to_dev(rdo, dev)
+            dst = torch.zeros(int(rdo[-1]) + 16, dtype=torch.uint8, device=dev)
+            st, fs, fl = codec.decode_fsm(src, so, do_t, dst)
+            do = rdo
+        torch.cuda.synchronize()
+        st = st.cpu().numpy()
+        assert np.array_equal(st, rst), tag
+        assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag
+        assert np.array_equal(fl.cpu().numpy(), rfl), tag
+        d = dst.cpu().numpy()
+        written = np.where(rst >= 0, rst, 0)
+        for i in range(n):
+            # compare every byte the oracle wrote (also on failure: the
+            # oracle's slot pool is zero-initialised like ours)
+            k = int(rdo[i + 1] - rdo[i]) if variant == "fsm" else int(written[i])
+            assert bytes(d[do[i]:do[i] + k]) == bytes(rd[rdo[i]:rdo[i] + k]), (tag, i)
+
+
+def test_fsm_streaming_chunks(codec, dev):
+    """Chunked decode through the batched FSM kernel, carrying the decode
+    context between calls (fin=0 then fin=1), equals whole-string decode --
+    the streaming contract of tests/nghttp2_test_helper.c:165-205."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off, _ = W.gen_adversarial(6000, seed=41)
+    n = len(off) - 1
+    lens = np.diff(off.astype(np.int64))
+    rng = np.random.default_rng(2)
+    cut = (rng.random(n) * (lens + 1)).astype(np.int64)
+    rd, rdo, rst, rfs, rfl = O.decode_batch(pool, off)
+    outs = []
+    state = flags = None
+    for part in range(2):
+        lo = np.where(part == 0, 0, cut)
+        hi = np.where(part == 0, cut, lens)
+        plen = hi - lo
+        chunks = np.concatenate([pool[off[i] + lo[i]: off[i] + hi[i]] for i in range(n)]) \
+            if plen.sum() else np.zeros(0, np.uint8)
+        cpool, coff = W._pool_from_lengths(plen, chunks)
+        slots = np.zeros(n + 1, dtype=np.int64)
+        slots[1:] = np.cumsum(plen * 8 // 5 + 1)
+        dst = torch.zeros(int(slots[-1]) + 16, dtype=torch.uint8, device=dev)
+        st, fs, fl = codec.decode_fsm(to_dev(cpool, dev), to_dev(coff, dev),
+                                      to_dev(slots.astype(np.uint32), dev), dst,
+                                      init_fstate=state, init_flags=flags, final=(part == 1))
+        torch.cuda.synchronize()
+        d = dst.cpu().numpy()
+        stn = st.cpu().numpy()
+        outs.append([bytes(d[slots[i]:slots[i] + max(0, stn[i])]) if part == 0 or stn[i] >= 0
+                     else None for i in range(n)])
+        state, flags = fs, fl
+    assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs)
+    assert np.array_equal(fl.cpu().numpy(), rfl)
+    assert np.array_equal(np.where(stn < 0, stn, 0), np.where(rst < 0, rst, 0))
+    for i in range(n):
+        if rst[i] >= 0:
+            assert outs[0][i] + outs[1][i] == bytes(rd[rdo[i]:rdo[i] + rst[i]]), i
