@@ -73,7 +73,7 @@ size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n);
 
 /* Size of the decode output pool nghttp2_amd_hd_huff_decode_batch_auto needs
  * for an encoded pool of `enc_bytes` bytes in `n` strings:
- * floor(8 * enc_bytes / 5) + n, rounded up. */
+ * floor(8 * enc_bytes / 5) + 4 * n, rounded up. */
 size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n);
 
 /* Bytes of device workspace nghttp2_amd_hd_huff_encode_batch and
@@ -157,11 +157,13 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
 
 /*
  * Same as nghttp2_amd_hd_huff_decode_batch, with the engine assigning the
- * output slots in the same launch: dst_off[i] = floor(8*(src_off[i] -
- * src_off[0])/5) + i (OUT, n+1 entries).  Each slot holds at least
- * floor(8*E_i/5)+1 bytes -- the reference's allocation -- so no string can
- * overflow; dst_cap must be >= nghttp2_amd_hd_huff_decode_bound(E_total, n)
- * (strings whose slot would end past dst_cap get -502 and write nothing).
+ * output slots in the same launch: with x_i = src_off[i] - src_off[0],
+ * dst_off[i] = 4 * (ceil(floor(8 x_i / 5) / 4) + i) (OUT, n+1 entries).
+ * Slots are 4-byte aligned and each holds at least floor(8*E_i/5)+1 bytes
+ * -- the reference's allocation -- so no string can overflow; bytes of a
+ * slot past its decoded length are unspecified.  dst (16-byte aligned) must
+ * hold nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes; strings whose slot
+ * would end past dst_cap get -502 and write nothing.
  */
 int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint8_t *dst, size_t dst_cap,

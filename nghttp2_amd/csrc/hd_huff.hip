@@ -321,20 +321,58 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T) {
   __syncthreads();
 }
 
-// Decode one string [a, b) into out.  Returns status; *fs / *fl receive the
-// final reference decode context (lib/nghttp2_hd_huffman.h:56-60).
-template <bool CHECK>
-__device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t *__restrict__ src,
-                                              uint32_t a, uint32_t b, uint8_t *__restrict__ dst,
-                                              uint32_t cap, uint32_t *fs, uint32_t *fl) {
+// Output writers for decode_one.  ByteSink: caller slots at any byte
+// alignment (ByteOut, capacity-checked).  WordSink: engine slots, 4-byte
+// aligned with room for align4(len), so symbols are packed four to a dword
+// and every store is a full aligned dword with no branch on alignment.
+struct ByteSink {
   ByteOut out;
-  out.init(dst);
+  uint32_t cap;
+  bool ovf;
+  __device__ __forceinline__ void init(uint8_t *p, uint32_t c) { out.init(p); cap = c; ovf = false; }
+  __device__ __forceinline__ void emit(uint32_t bytes, uint32_t cnt, uint32_t nsym) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+      if (nsym + i < cap) out.put((bytes >> (8 * i)) & 0xFFu); else ovf = true;
+    }
+  }
+  __device__ __forceinline__ void finish() { out.flush(); }
+};
+
+struct WordSink {
+  uint32_t *p;
+  uint32_t acc, k;
+  bool ovf;
+  __device__ __forceinline__ void init(uint8_t *q, uint32_t) {
+    p = reinterpret_cast<uint32_t *>(q); acc = 0; k = 0; ovf = false;
+  }
+  // append cnt (0..2) bytes, little-endian in `bytes` (higher bytes zero)
+  __device__ __forceinline__ void emit(uint32_t bytes, uint32_t cnt, uint32_t) {
+    uint64_t t = (uint64_t)acc | ((uint64_t)bytes << (8 * k));
+    k += cnt;
+    if (k >= 4) {
+      *p++ = (uint32_t)t;
+      t >>= 32;
+      k -= 4;
+    }
+    acc = (uint32_t)t;
+  }
+  __device__ __forceinline__ void finish() {
+    if (k) *p = acc;
+  }
+};
+
+// Decode one string [a, b) into sink.  Returns status; *fs / *fl receive the
+// final reference decode context (lib/nghttp2_hd_huffman.h:56-60).
+template <class Sink>
+__device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t *__restrict__ src,
+                                              uint32_t a, uint32_t b, Sink &sink,
+                                              uint32_t *fs, uint32_t *fl) {
   uint64_t bb = 0;   // MSB-aligned bit buffer
   uint32_t nb = 0;   // valid bits in bb
   uint32_t pos = a;  // next byte to load
   uint32_t rem = 8u * (b - a);  // bits of the string not yet decoded
   uint32_t nsym = 0;
-  bool failed = false, ovf = false;
+  bool failed = false;
   while (rem) {
     if (nb <= 32 && pos < b) {
       const uint32_t x = load_be32(src, pos, b);
@@ -343,46 +381,44 @@ __device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t 
       nb += 8 * v;
       pos += v;
     }
-    const uint32_t e = T.lut[(uint32_t)(bb >> (64 - HD_HUFF_LUT_BITS))];
-    uint32_t L1 = (e >> 16) & 15u;
-    uint32_t sym;
-    if (L1 == 0) {
-      // code longer than the lookup: canonical length by left-justified limits
+    uint32_t e = T.lut[(uint32_t)(bb >> (64 - HD_HUFF_LUT_BITS))];
+    if ((e & 0xF0000u) == 0) {
+      // code longer than the lookup (rare): canonical length by
+      // left-justified limits, then the symbol; re-encode as a 1-symbol entry
       const uint32_t win = (uint32_t)(bb >> 32);
-      uint32_t first = 0, base = 0;
+      uint32_t L = 0, first = 0, base = 0;
 #define HD_LONG_STEP(LEN, LIM, FIRST, BASE) \
-      if (L1 == 0 && (uint64_t)win < (LIM)) { L1 = (LEN); first = (FIRST); base = (BASE); }
+      if (L == 0 && (uint64_t)win < (LIM)) { L = (LEN); first = (FIRST); base = (BASE); }
       HD_HUFF_LONG_CODES(HD_LONG_STEP)
 #undef HD_LONG_STEP
-      if (L1 > rem) break;
-      sym = T.canon[base + ((win >> (32 - L1)) - first)];
-      if (sym == 256) {  // EOS decoded: the FSM's sticky failure state
-        failed = true;
-        break;
+      uint32_t sym = 0;
+      if (L <= rem) {
+        sym = T.canon[base + ((win >> (32 - L)) - first)];
+        if (sym == 256) {  // EOS decoded: the FSM's sticky failure state
+          failed = true;
+          break;
+        }
       }
-    } else {
-      if (L1 > rem) break;
-      sym = e & 0xFFu;
+      e = sym | (L << 16);  // L may be 16..30: bits 16..20
     }
-    if (!CHECK || nsym < cap) out.put(sym); else ovf = true;
-    ++nsym;
-    bb <<= L1;
-    nb -= L1;
-    rem -= L1;
-    const uint32_t L2 = (e >> 20) & 15u;
-    if (L2 && L2 <= rem) {
-      if (!CHECK || nsym < cap) out.put((e >> 8) & 0xFFu); else ovf = true;
-      ++nsym;
-      bb <<= L2;
-      nb -= L2;
-      rem -= L2;
-    }
+    const uint32_t L1 = (e >> 16) & 31u;
+    const uint32_t L2 = (e >> 21) & 15u;
+    const bool ok1 = L1 <= rem;
+    const bool ok2 = ok1 && L2 != 0 && L1 + L2 <= rem;
+    const uint32_t cnt = (uint32_t)ok1 + (uint32_t)ok2;
+    sink.emit(ok1 ? (e & (ok2 ? 0xFFFFu : 0xFFu)) : 0u, cnt, nsym);
+    const uint32_t used = ok1 ? (ok2 ? L1 + L2 : L1) : 0u;
+    nsym += cnt;
+    bb <<= used;
+    nb -= used;
+    rem -= used;
+    if (!ok1) break;
   }
-  out.flush();
+  sink.finish();
   if (failed) {
     *fs = FAIL_STATE;
     *fl = 0;
-    return CHECK && ovf ? NGHTTP2_AMD_ERR_BUFFER_ERROR : NGHTTP2_AMD_ERR_HEADER_COMP;
+    return sink.ovf ? NGHTTP2_AMD_ERR_BUFFER_ERROR : NGHTTP2_AMD_ERR_HEADER_COMP;
   }
   // tail = the last `rem` (< 30) bits: a proper prefix of a code, i.e. an
   // internal node of the code tree -> the FSM state it leaves behind.
@@ -391,13 +427,21 @@ __device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t 
   const bool accept = (t <= 7) && (v == (1u << t) - 1u);
   *fs = t ? T.depth_ids[T.depth_base[t] + (v - T.depth_lo[t])] : 0u;
   *fl = (accept ? HUFF_ACCEPTED : 0u) | ((t < 4 && nsym) ? HUFF_SYM : 0u);
-  if (CHECK && ovf) return NGHTTP2_AMD_ERR_BUFFER_ERROR;
+  if (sink.ovf) return NGHTTP2_AMD_ERR_BUFFER_ERROR;
   return accept ? (int32_t)nsym : NGHTTP2_AMD_ERR_HEADER_COMP;
 }
 
-// AUTO: the engine assigns slots dst_off[s] = floor(8 (off[s]-off[0]) / 5)
-// + s (>= the reference's floor(8E/5)+1 per string, so no check needed) and
-// writes them out; else caller slots, capacity-checked.
+// Engine slot layout (AUTO): slot_s = 4 * (ceil(floor(8 x_s / 5) / 4) + s)
+// with x_s = off[s] - off[0].  Every slot is 4-byte aligned and holds at
+// least floor(8 E_s / 5) + 1 bytes (the reference's allocation,
+// lib/nghttp2_hd.c:2080-2082) rounded up to a whole dword.
+__device__ __host__ __forceinline__ uint64_t auto_slot(uint32_t x, uint32_t s) {
+  const uint64_t g = ((uint64_t)x * 8u) / 5u;
+  return 4u * (((g + 3u) >> 2) + s);
+}
+
+// AUTO: engine-assigned slots (written out to dst_off); else caller slots,
+// capacity-checked.
 template <bool AUTO>
 __global__ __launch_bounds__(WG) void k_decode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
@@ -411,24 +455,25 @@ __global__ __launch_bounds__(WG) void k_decode(const uint8_t *__restrict__ src,
   const uint32_t off0 = off[0];
   for (uint32_t s = blockIdx.x * WG + threadIdx.x; s < n; s += gridDim.x * WG) {
     const uint32_t a = off[s], b = off[s + 1];
-    uint32_t o, cap;
+    uint32_t fs, fl;
+    int32_t st;
     if (AUTO) {
-      const uint64_t o64 = ((uint64_t)(a - off0) * 8u) / 5u + s;
-      const uint64_t e64 = ((uint64_t)(b - off0) * 8u) / 5u + s + 1;
-      o = (uint32_t)o64;
-      cap = (uint32_t)(e64 - o64);
-      dst_off[s] = o;
-      if (s == n - 1) dst_off[n] = (uint32_t)e64;
-      if (e64 > dst_cap) {
+      const uint64_t o64 = auto_slot(a - off0, s);
+      dst_off[s] = (uint32_t)o64;
+      if (s == n - 1) dst_off[n] = (uint32_t)auto_slot(b - off0, n);
+      if (auto_slot(b - off0, s + 1) > dst_cap) {
         status[s] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
         continue;
       }
+      WordSink sink;
+      sink.init(dst + o64, 0);
+      st = decode_one(T, src, a, b, sink, &fs, &fl);
     } else {
-      o = dst_off[s];
-      cap = dst_off[s + 1] - o;
+      const uint32_t o = dst_off[s];
+      ByteSink sink;
+      sink.init(dst + o, dst_off[s + 1] - o);
+      st = decode_one(T, src, a, b, sink, &fs, &fl);
     }
-    uint32_t fs, fl;
-    const int32_t st = decode_one<!AUTO>(T, src, a, b, dst + o, cap, &fs, &fl);
     status[s] = st;
     if (fstate_out) fstate_out[s] = (uint16_t)fs;
     if (flags_out) flags_out[s] = (uint8_t)fl;
@@ -488,9 +533,24 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
 // C ABI
 // ---------------------------------------------------------------------------
 static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
-static inline uint32_t persistent_grid(uint32_t n) {
-  uint32_t g = ntiles_for(n);
-  return g < NUM_CU * DEC_WG_PER_CU ? g : NUM_CU * DEC_WG_PER_CU;
+// Persistent grids are sized to what is resident at once (occupancy query
+// x CU count, cached per kernel), so no workgroup runs as a second "wave"
+// and the LDS tables are staged once per resident workgroup.
+template <class K>
+static uint32_t resident_blocks(K kernel) {
+  int dev = 0, cus = NUM_CU, per = DEC_WG_PER_CU;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WG, 0) != hipSuccess || per < 1)
+    per = 1;
+  return (uint32_t)(cus * per);
+}
+template <auto KERNEL>
+static uint32_t persistent_grid(uint32_t n) {
+  static uint32_t cap = 0;  // one per kernel
+  if (cap == 0) cap = resident_blocks(KERNEL);
+  const uint32_t g = ntiles_for(n);
+  return g < cap ? g : cap;
 }
 
 static int hip_rv(hipError_t e) {
@@ -521,7 +581,7 @@ size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n) {
 }
 
 size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n) {
-  uint64_t b = (enc_bytes * 8u) / 5u + (uint64_t)n + 16u;
+  uint64_t b = (enc_bytes * 8u) / 5u + 4u * (uint64_t)n + 16u;
   return (size_t)((b + 15u) & ~(uint64_t)15u);
 }
 
@@ -580,7 +640,7 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                                      void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid(n)), dim3(WG), 0,
+  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid<k_decode<false>>(n)), dim3(WG), 0,
                      (hipStream_t)stream, src, src_off, n, dst, (uint64_t)0,
                      (uint32_t *)dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
@@ -594,7 +654,7 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid(n)), dim3(WG), 0, st, src, src_off,
+  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>>(n)), dim3(WG), 0, st, src, src_off,
                      n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
 }
@@ -608,7 +668,7 @@ int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((init_fstate == nullptr) != (init_flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode_fsm, dim3(persistent_grid(n)), dim3(WG), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_decode_fsm, dim3(persistent_grid<k_decode_fsm>(n)), dim3(WG), 0, (hipStream_t)stream,
                      src, src_off, n, dst, dst_off, status, fstate, flags, init_fstate,
                      init_flags, final);
   return hip_rv(hipGetLastError());

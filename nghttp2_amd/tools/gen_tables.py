@@ -167,7 +167,7 @@ def build():
     # 12-bit multi-symbol lookup table for the canonical decoder: for every
     # 12-bit window, the first code if it is <= 12 bits (sym1, L1) and, when
     # the rest of the window holds another whole code, the second (sym2, L2).
-    # Entry: sym1 | sym2 << 8 | L1 << 16 | L2 << 20; L1 == 0 means the first
+    # Entry: sym1 | sym2 << 8 | L1 << 16 | L2 << 21; L1 == 0 means the first
     # code is longer than 12 bits (all such codes start with >= 10 ones).
     lut = []
     for w in range(1 << LUT_BITS):
@@ -185,7 +185,7 @@ def build():
             s2, L2 = first_code(w & ((1 << r) - 1), r) if r else (None, 0)
             e = s1 | (L1 << 16)
             if s2 is not None:
-                e |= (s2 << 8) | (L2 << 20)
+                e |= (s2 << 8) | (L2 << 21)
         lut.append(e)
     # long codes: (L, left-justified exclusive limit as a 32-bit-window
     # compare, first code, canonical index base) for every length > LUT_BITS
@@ -253,7 +253,7 @@ def write_inc(t, path):
     for i in range(0, 256, 16):
         w("  " + ", ".join("%d" % v for v in t["id_list"][i:i + 16]) + ",")
     w("};")
-    w("/* canonical decoder: %d-bit lookup, sym1 | sym2 << 8 | L1 << 16 | L2 << 20 */" % LUT_BITS)
+    w("/* canonical decoder: %d-bit lookup, sym1 | sym2 << 8 | L1 << 16 | L2 << 21 */" % LUT_BITS)
     w("#define HD_HUFF_LUT_BITS %d" % LUT_BITS)
     w("HD_TBL const unsigned int hd_huff_lut[%d] = {" % (1 << LUT_BITS))
     for i in range(0, 1 << LUT_BITS, 8):
