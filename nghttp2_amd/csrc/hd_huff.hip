@@ -45,6 +45,9 @@ namespace host {
 #define SCAN_WG 1024
 #define DEC_WG_PER_CU 8 // persistent decode grid: 256 CUs x 8 workgroups
 #define NUM_CU 256
+#define ENC_OBUF 16384  // LDS output staging per encode workgroup (bytes)
+#define DEC_WG 512      // decode workgroup: 8 waves share one table copy
+#define DEC_OBUF 32768  // LDS output staging per decode workgroup (bytes)
 
 #define HUFF_ACCEPTED 0x01u
 #define HUFF_SYM 0x02u
@@ -109,27 +112,36 @@ struct ByteOut {
   }
 };
 
+// Address-space-explicit pointers, so LDS staging compiles to ds_* and
+// global output to global_* (never flat_*).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+template <class BP> struct W32Of { typedef uint32_t type; };
+template <> struct W32Of<lds_u8 *> { typedef lds_u32 type; };
+template <class BP> using W32 = typename W32Of<BP>::type;
+
 // Word writer for encode output: the stream [o, o+E) receives big-endian
 // 32-bit groups; with phase = o & 3 fixed, each group completes one aligned
 // word (funnel shift with the pending bytes).  The head word that also holds
 // the previous string's bytes, and the tail, are written byte by byte.
+template <class BP>  // BP: byte pointer (global or LDS address space)
 struct WordOut {
-  uint8_t *base;
+  BP base;
   uint32_t q, o, phase, pend;
-  __device__ __forceinline__ void init(uint8_t *b, uint32_t start) {
+  __device__ __forceinline__ void init(BP b, uint32_t start) {
     base = b; q = start; o = start; phase = start & 3u; pend = 0;
   }
   __device__ __forceinline__ void put32(uint32_t be) {
     const uint32_t le = __builtin_bswap32(be);
     if (phase == 0) {
-      *reinterpret_cast<uint32_t *>(base + q) = le;
+      *reinterpret_cast<W32<BP> *>(base + q) = le;
     } else {
       const uint32_t word = pend | (le << (8 * phase));
       const uint32_t wa = q & ~3u;
       if (wa < o) {
         for (uint32_t k = phase; k < 4; ++k) base[wa + k] = (uint8_t)(word >> (8 * k));
       } else {
-        *reinterpret_cast<uint32_t *>(base + wa) = word;
+        *reinterpret_cast<W32<BP> *>(base + wa) = word;
       }
       pend = le >> (8 * (4 - phase));
     }
@@ -253,27 +265,15 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 // ---------------------------------------------------------------------------
 // encode, pass 2: bit packing   (lib/nghttp2_hd_huffman.c:45-104)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
-                                               const uint32_t *__restrict__ off, uint32_t n,
-                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
-                                               uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_prefix) {
-  __shared__ uint2 codeT[256];
-  __shared__ uint32_t red[WG / 64];
-  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x],
-                                  dev::hd_huff_enc_len[threadIdx.x]);
-  const uint32_t s = blockIdx.x * WG + threadIdx.x;
-  const uint32_t E = (s < n) ? dst_off[s] : 0u;
-  uint32_t tot;
-  const uint32_t o = tile_prefix[blockIdx.x] + block_excl_scan<WG>(E, red, &tot);
-  if (s >= n) return;
-  dst_off[s] = o;
-  if ((uint64_t)o + E > dst_cap) return;  // never write past the pool
-  const uint32_t a = off[s], b = off[s + 1];
+// Bit-pack one string [a, b) MSB-first (lib/nghttp2_hd_huffman.c:57-84) into
+// out_base[o ..], padding the last byte with the EOS prefix (:95-101).
+template <class BP>
+__device__ __forceinline__ void encode_one(const uint2 *codeT, const uint8_t *__restrict__ src,
+                                           uint32_t a, uint32_t b, BP out_base, uint32_t o) {
   uint64_t acc = 0;  // MSB-aligned pending bits, nb < 32 between bytes
   uint32_t nb = 0;
-  WordOut out;
-  out.init(dst, o);
+  WordOut<BP> out;
+  out.init(out_base, o);
   for (uint32_t c = a & ~15u; c < b; c += 16) {
     const uint4 v = *reinterpret_cast<const uint4 *>(src + c);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -292,32 +292,94 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
       }
     }
   }
-  // pad the last partial byte with the EOS prefix (all ones), :95-101
   const uint32_t pad = (8u - (nb & 7u)) & 7u;
   acc |= (~0ull >> nb) & ~(~0ull >> (nb + pad));
   nb += pad;
   out.finish((uint32_t)(acc >> 32), nb >> 3);
 }
 
+__global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
+                                               const uint32_t *__restrict__ off, uint32_t n,
+                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                               uint32_t *__restrict__ dst_off,
+                                               const uint32_t *__restrict__ tile_prefix) {
+  __shared__ uint2 codeT[256];
+  __shared__ uint32_t red[WG / 64];
+  __shared__ uint32_t obuf[ENC_OBUF / 4];
+  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x],
+                                  dev::hd_huff_enc_len[threadIdx.x]);
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  const uint32_t E = (s < n) ? dst_off[s] : 0u;
+  uint32_t tot;
+  const uint32_t O0 = tile_prefix[blockIdx.x];
+  const uint32_t o = O0 + block_excl_scan<WG>(E, red, &tot);
+  const uint32_t Oend = O0 + tot;
+  const uint32_t base = O0 & ~3u;
+  // The tile's output [O0, Oend) is contiguous: stage it in LDS and store it
+  // with coalesced dwords (byte stores only for the two edge words shared
+  // with the neighbouring tiles).  Uniform across the workgroup.
+  const bool staged = (Oend - base) <= ENC_OBUF && (uint64_t)Oend <= dst_cap;
+  if (s < n) {
+    dst_off[s] = o;
+    if (staged) {
+      encode_one(codeT, src, off[s], off[s + 1], (lds_u8 *)obuf, o - base);
+    } else if ((uint64_t)o + E <= dst_cap) {  // never write past the pool
+      encode_one(codeT, src, off[s], off[s + 1], dst, o);
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    const uint32_t nwords = (Oend - base + 3u) >> 2;
+    for (uint32_t i = threadIdx.x; i < nwords; i += WG) {
+      const uint32_t ga = base + 4u * i;
+      const uint32_t w = obuf[i];
+      if (ga >= O0 && ga + 4u <= Oend) {
+        *reinterpret_cast<uint32_t *>(dst + ga) = w;
+      } else {
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t q = ga + k;
+          if (q >= O0 && q < Oend) dst[q] = (uint8_t)(w >> (8 * k));
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // decode: canonical multi-symbol decoder
 // ---------------------------------------------------------------------------
+#define NLONG 14  // code lengths > HD_HUFF_LUT_BITS (13,14,15,19..28,30)
+
 struct DecTables {
   uint32_t lut[1 << HD_HUFF_LUT_BITS];
+  uint32_t long_lim[NLONG];    // exclusive left-justified limit (last: ~0)
+  uint32_t long_delta[NLONG];  // canonical base - first code (mod 2^32)
+  uint32_t long_len[NLONG];
   uint16_t canon[260];
   uint32_t depth_lo[30];
   uint16_t depth_base[30];
   uint8_t depth_ids[256];
 };
 
-__device__ __forceinline__ void stage_dec_tables(DecTables &T) {
-  for (uint32_t i = threadIdx.x; i < (1u << HD_HUFF_LUT_BITS); i += WG) T.lut[i] = dev::hd_huff_lut[i];
-  for (uint32_t i = threadIdx.x; i < 257; i += WG) T.canon[i] = dev::hd_huff_canon_sym[i];
-  if (threadIdx.x < 30) {
-    T.depth_lo[threadIdx.x] = dev::hd_huff_depth_lo[threadIdx.x];
-    T.depth_base[threadIdx.x] = dev::hd_huff_depth_base[threadIdx.x];
+__device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < (1u << HD_HUFF_LUT_BITS); i += nthreads) T.lut[i] = dev::hd_huff_lut[i];
+  for (uint32_t i = t; i < 257; i += nthreads) T.canon[i] = dev::hd_huff_canon_sym[i];
+  if (t < 30) {
+    T.depth_lo[t] = dev::hd_huff_depth_lo[t];
+    T.depth_base[t] = dev::hd_huff_depth_base[t];
   }
-  T.depth_ids[threadIdx.x] = dev::hd_huff_depth_ids[threadIdx.x];
+  if (t < 256) T.depth_ids[t] = dev::hd_huff_depth_ids[t];
+  if (t == 0) {
+    uint32_t i = 0;
+#define HD_LONG_ROW(LEN, LIM, FIRST, BASE)                                    \
+    T.long_lim[i] = (LIM) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(LIM);   \
+    T.long_delta[i] = (uint32_t)(BASE) - (uint32_t)(FIRST);                  \
+    T.long_len[i] = (LEN);                                                   \
+    ++i;
+    HD_HUFF_LONG_CODES(HD_LONG_ROW)
+#undef HD_LONG_ROW
+  }
   __syncthreads();
 }
 
@@ -338,13 +400,12 @@ struct ByteSink {
   __device__ __forceinline__ void finish() { out.flush(); }
 };
 
+template <class WP>  // WP: dword pointer (global or LDS address space)
 struct WordSink {
-  uint32_t *p;
+  WP p;
   uint32_t acc, k;
   bool ovf;
-  __device__ __forceinline__ void init(uint8_t *q, uint32_t) {
-    p = reinterpret_cast<uint32_t *>(q); acc = 0; k = 0; ovf = false;
-  }
+  __device__ __forceinline__ void init(WP q) { p = q; acc = 0; k = 0; ovf = false; }
   // append cnt (0..2) bytes, little-endian in `bytes` (higher bytes zero)
   __device__ __forceinline__ void emit(uint32_t bytes, uint32_t cnt, uint32_t) {
     uint64_t t = (uint64_t)acc | ((uint64_t)bytes << (8 * k));
@@ -383,23 +444,27 @@ __device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t 
     }
     uint32_t e = T.lut[(uint32_t)(bb >> (64 - HD_HUFF_LUT_BITS))];
     if ((e & 0xF0000u) == 0) {
-      // code longer than the lookup (rare): canonical length by
-      // left-justified limits, then the symbol; re-encode as a 1-symbol entry
+      // code longer than the lookup (rare): canonical length by binary
+      // search over the left-justified limits, then the symbol
       const uint32_t win = (uint32_t)(bb >> 32);
-      uint32_t L = 0, first = 0, base = 0;
-#define HD_LONG_STEP(LEN, LIM, FIRST, BASE) \
-      if (L == 0 && (uint64_t)win < (LIM)) { L = (LEN); first = (FIRST); base = (BASE); }
-      HD_HUFF_LONG_CODES(HD_LONG_STEP)
-#undef HD_LONG_STEP
+      uint32_t lo = 0, hi = NLONG - 1;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lo < hi) {
+          if (win < T.long_lim[mid]) hi = mid; else lo = mid + 1;
+        }
+      }
+      const uint32_t L = T.long_len[lo];
       uint32_t sym = 0;
       if (L <= rem) {
-        sym = T.canon[base + ((win >> (32 - L)) - first)];
+        sym = T.canon[(win >> (32 - L)) + T.long_delta[lo]];
         if (sym == 256) {  // EOS decoded: the FSM's sticky failure state
           failed = true;
           break;
         }
       }
-      e = sym | (L << 16);  // L may be 16..30: bits 16..20
+      e = sym | (L << 16);  // L up to 30: bits 16..20
     }
     const uint32_t L1 = (e >> 16) & 31u;
     const uint32_t L2 = (e >> 21) & 15u;
@@ -440,43 +505,99 @@ __device__ __host__ __forceinline__ uint64_t auto_slot(uint32_t x, uint32_t s) {
   return 4u * (((g + 3u) >> 2) + s);
 }
 
-// AUTO: engine-assigned slots (written out to dst_off); else caller slots,
-// capacity-checked.
+// Length-sorted lane assignment inside a tile of NT strings: a stable
+// counting sort of the strings by (bucketed) encoded length, so each wave
+// decodes strings of similar length and no lane idles for long while its
+// wave's longest string finishes.  Returns the tile-relative string index
+// this lane decodes (>= cnt: none).
+template <int NT>
+__device__ __forceinline__ uint32_t sorted_lane(uint32_t len, bool live, uint32_t *hist,
+                                                uint16_t *perm, uint32_t *red) {
+  const uint32_t t = threadIdx.x;
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  const uint32_t bkt = len < 192u ? len : min(255u, 192u + ((len - 192u) >> 4));
+  uint32_t rank = 0;
+  if (live) rank = atomicAdd(&hist[bkt], 1u);
+  __syncthreads();
+  const uint32_t h = (t < 256) ? hist[t] : 0u;
+  uint32_t tot;
+  const uint32_t start = block_excl_scan<NT>(h, red, &tot);
+  if (t < 256) hist[t] = start;
+  __syncthreads();
+  if (live) perm[hist[bkt] + rank] = (uint16_t)t;
+  __syncthreads();
+  return (t < tot) ? (uint32_t)perm[t] : 0xFFFFFFFFu;
+}
+
+// AUTO: engine-assigned slots (written out to dst_off), the tile's slots
+// staged in LDS and stored with coalesced dwords when they fit; else caller
+// slots, capacity-checked, written directly.
 template <bool AUTO>
-__global__ __launch_bounds__(WG) void k_decode(const uint8_t *__restrict__ src,
-                                               const uint32_t *__restrict__ off, uint32_t n,
-                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
-                                               uint32_t *__restrict__ dst_off,
-                                               int32_t *__restrict__ status,
-                                               uint16_t *__restrict__ fstate_out,
-                                               uint8_t *__restrict__ flags_out) {
+__global__ __launch_bounds__(DEC_WG) void k_decode(const uint8_t *__restrict__ src,
+                                                   const uint32_t *__restrict__ off, uint32_t n,
+                                                   uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                                   uint32_t *__restrict__ dst_off,
+                                                   int32_t *__restrict__ status,
+                                                   uint16_t *__restrict__ fstate_out,
+                                                   uint8_t *__restrict__ flags_out) {
   __shared__ DecTables T;
-  stage_dec_tables(T);
+  __shared__ uint32_t obuf[AUTO ? DEC_OBUF / 4 : 1];
+  __shared__ uint32_t hist[256];
+  __shared__ uint16_t perm[DEC_WG];
+  __shared__ uint32_t red[DEC_WG / 64];
+  stage_dec_tables(T, DEC_WG);
   const uint32_t off0 = off[0];
-  for (uint32_t s = blockIdx.x * WG + threadIdx.x; s < n; s += gridDim.x * WG) {
-    const uint32_t a = off[s], b = off[s + 1];
-    uint32_t fs, fl;
-    int32_t st;
+  for (uint32_t t0 = blockIdx.x * DEC_WG; t0 < n; t0 += gridDim.x * DEC_WG) {
+    const uint32_t mine = t0 + threadIdx.x;
+    const bool live0 = mine < n;
+    const uint32_t len0 = live0 ? off[mine + 1] - off[mine] : 0u;
+    const uint32_t r = sorted_lane<DEC_WG>(len0, live0, hist, perm, red);
+    const uint32_t s = t0 + r;
+    const bool live = r != 0xFFFFFFFFu;
+    uint32_t fs = 0, fl = 0;
+    int32_t st = 0;
     if (AUTO) {
-      const uint64_t o64 = auto_slot(a - off0, s);
-      dst_off[s] = (uint32_t)o64;
-      if (s == n - 1) dst_off[n] = (uint32_t)auto_slot(b - off0, n);
-      if (auto_slot(b - off0, s + 1) > dst_cap) {
-        status[s] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
-        continue;
+      const uint32_t s1 = min(t0 + DEC_WG, n);
+      const uint64_t lo = auto_slot(off[t0] - off0, t0);
+      const uint64_t hi = auto_slot(off[s1] - off0, s1);
+      const bool staged = (hi - lo) <= DEC_OBUF && hi <= dst_cap;  // uniform
+      if (live) {
+        const uint32_t a = off[s], b = off[s + 1];
+        const uint64_t o64 = auto_slot(a - off0, s);
+        dst_off[s] = (uint32_t)o64;
+        if (s == n - 1) dst_off[n] = (uint32_t)auto_slot(b - off0, n);
+        if (staged) {
+          WordSink<lds_u32 *> sink;
+          sink.init((lds_u32 *)obuf + ((o64 - lo) >> 2));
+          st = decode_one(T, src, a, b, sink, &fs, &fl);
+        } else if (auto_slot(b - off0, s + 1) > dst_cap) {
+          st = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+        } else {
+          WordSink<uint32_t *> sink;
+          sink.init(reinterpret_cast<uint32_t *>(dst + o64));
+          st = decode_one(T, src, a, b, sink, &fs, &fl);
+        }
       }
-      WordSink sink;
-      sink.init(dst + o64, 0);
-      st = decode_one(T, src, a, b, sink, &fs, &fl);
-    } else {
+      if (staged) {
+        __syncthreads();
+        const uint32_t nwords = (uint32_t)((hi - lo) >> 2);
+        uint32_t *g = reinterpret_cast<uint32_t *>(dst + lo);
+        for (uint32_t i = threadIdx.x; i < nwords; i += DEC_WG) g[i] = obuf[i];
+      }
+    } else if (live) {
+      const uint32_t a = off[s], b = off[s + 1];
       const uint32_t o = dst_off[s];
       ByteSink sink;
       sink.init(dst + o, dst_off[s + 1] - o);
       st = decode_one(T, src, a, b, sink, &fs, &fl);
     }
-    status[s] = st;
-    if (fstate_out) fstate_out[s] = (uint16_t)fs;
-    if (flags_out) flags_out[s] = (uint8_t)fl;
+    if (live) {
+      status[s] = st;
+      if (fstate_out) fstate_out[s] = (uint16_t)fs;
+      if (flags_out) flags_out[s] = (uint8_t)fl;
+    }
+    __syncthreads();  // obuf / hist / perm reuse by the next tile
   }
 }
 
@@ -533,23 +654,24 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
 // C ABI
 // ---------------------------------------------------------------------------
 static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
+static inline uint32_t ntiles_dec(uint32_t n) { return (n + DEC_WG - 1) / DEC_WG; }
 // Persistent grids are sized to what is resident at once (occupancy query
 // x CU count, cached per kernel), so no workgroup runs as a second "wave"
 // and the LDS tables are staged once per resident workgroup.
 template <class K>
-static uint32_t resident_blocks(K kernel) {
+static uint32_t resident_blocks(K kernel, int BS) {
   int dev = 0, cus = NUM_CU, per = DEC_WG_PER_CU;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WG, 0) != hipSuccess || per < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, BS, 0) != hipSuccess || per < 1)
     per = 1;
   return (uint32_t)(cus * per);
 }
-template <auto KERNEL>
+template <auto KERNEL, int BS>
 static uint32_t persistent_grid(uint32_t n) {
   static uint32_t cap = 0;  // one per kernel
-  if (cap == 0) cap = resident_blocks(KERNEL);
-  const uint32_t g = ntiles_for(n);
+  if (cap == 0) cap = resident_blocks(KERNEL, BS);
+  const uint32_t g = (n + BS - 1) / BS;
   return g < cap ? g : cap;
 }
 
@@ -640,7 +762,7 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                                      void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid<k_decode<false>>(n)), dim3(WG), 0,
+  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid<k_decode<false>, DEC_WG>(n)), dim3(DEC_WG), 0,
                      (hipStream_t)stream, src, src_off, n, dst, (uint64_t)0,
                      (uint32_t *)dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
@@ -654,7 +776,7 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>>(n)), dim3(WG), 0, st, src, src_off,
+  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>, DEC_WG>(n)), dim3(DEC_WG), 0, st, src, src_off,
                      n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
 }
@@ -668,7 +790,7 @@ int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((init_fstate == nullptr) != (init_flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode_fsm, dim3(persistent_grid<k_decode_fsm>(n)), dim3(WG), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_decode_fsm, dim3(persistent_grid<k_decode_fsm, WG>(n)), dim3(WG), 0, (hipStream_t)stream,
                      src, src_off, n, dst, dst_off, status, fstate, flags, init_fstate,
                      init_flags, final);
   return hip_rv(hipGetLastError());

@@ -3,7 +3,7 @@
 # MI355X_MICROARCH.md prescribes) over a short bench run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 ARGS="${BENCH_ARGS:---no-cpu-baseline --steps 5 --warmup 2}"
 i=0
