@@ -48,6 +48,21 @@ namespace host {
 #define ENC_OBUF 16384  // LDS output staging per encode workgroup (bytes)
 #define DEC_WG 512      // decode workgroup: 8 waves share one table copy
 #define DEC_OBUF 32768  // LDS output staging per decode workgroup (bytes)
+#define DEC_IBUF 20480  // LDS input staging per decode workgroup (bytes)
+
+// Ablation switches (tools/diag builds variants; product uses defaults)
+#ifndef HD_DEC_INSTAGE
+#define HD_DEC_INSTAGE 1   // stage each decode tile's input bytes in LDS
+#endif
+#ifndef HD_DEC_SORT
+#define HD_DEC_SORT 1      // length-sorted lane assignment inside a tile
+#endif
+#ifndef HD_DEC_OUTSTAGE
+#define HD_DEC_OUTSTAGE 1  // stage the tile's output slots in LDS
+#endif
+#ifndef HD_DIAG_SKIP_LOOP
+#define HD_DIAG_SKIP_LOOP 0  // diagnostic only: no symbol decoding at all
+#endif
 
 #define HUFF_ACCEPTED 0x01u
 #define HUFF_SYM 0x02u
@@ -168,6 +183,14 @@ __device__ __forceinline__ uint32_t load_be32(const uint8_t *base, uint32_t pos,
   const uint32_t v = end - pos;
   if (v < 4) x &= ~(0xFFFFFFFFu >> (8 * v));
   return x;
+}
+
+// Same from an LDS staging buffer (byte index relative to the buffer, which
+// holds at least 8 readable bytes past every index used).
+__device__ __forceinline__ uint32_t load_be32_lds(const uint32_t *buf, uint32_t pos) {
+  const uint32_t w0 = buf[pos >> 2];
+  const uint32_t w1 = buf[(pos >> 2) + 1];
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
 }
 
 // ---------------------------------------------------------------------------
@@ -383,101 +406,140 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
   __syncthreads();
 }
 
-// Output writers for decode_one.  ByteSink: caller slots at any byte
-// alignment (ByteOut, capacity-checked).  WordSink: engine slots, 4-byte
-// aligned with room for align4(len), so symbols are packed four to a dword
-// and every store is a full aligned dword with no branch on alignment.
-struct ByteSink {
-  ByteOut out;
-  uint32_t cap;
+// Decode output sinks.  put2(e, cnt): append the cnt (1..2) symbol bytes in
+// the low 16 bits of e.  Engine-slot sinks write both bytes unconditionally
+// (a stray second byte is overwritten by the next symbol; every slot has a
+// spare byte past floor(8E/5)) -- no branch, no accumulator.
+template <class BP>  // BP: byte pointer (LDS or global)
+struct SlotSink {
+  BP p;
   bool ovf;
-  __device__ __forceinline__ void init(uint8_t *p, uint32_t c) { out.init(p); cap = c; ovf = false; }
-  __device__ __forceinline__ void emit(uint32_t bytes, uint32_t cnt, uint32_t nsym) {
+  __device__ __forceinline__ void init(BP q) { p = q; ovf = false; }
+  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
+    p[0] = (uint8_t)e;
+    p[1] = (uint8_t)(e >> 8);
+    p += cnt;
+  }
+  __device__ __forceinline__ void finish() {}
+};
+
+// Caller slots (any alignment, capacity checked): ByteOut-based.
+struct CheckedSink {
+  ByteOut out;
+  uint32_t cap, n;
+  bool ovf;
+  __device__ __forceinline__ void init(uint8_t *p, uint32_t c) {
+    out.init(p); cap = c; n = 0; ovf = false;
+  }
+  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
     for (uint32_t i = 0; i < cnt; ++i) {
-      if (nsym + i < cap) out.put((bytes >> (8 * i)) & 0xFFu); else ovf = true;
+      if (n < cap) out.put((e >> (8 * i)) & 0xFFu); else ovf = true;
+      ++n;
     }
   }
   __device__ __forceinline__ void finish() { out.flush(); }
 };
 
-template <class WP>  // WP: dword pointer (global or LDS address space)
-struct WordSink {
-  WP p;
-  uint32_t acc, k;
-  bool ovf;
-  __device__ __forceinline__ void init(WP q) { p = q; acc = 0; k = 0; ovf = false; }
-  // append cnt (0..2) bytes, little-endian in `bytes` (higher bytes zero)
-  __device__ __forceinline__ void emit(uint32_t bytes, uint32_t cnt, uint32_t) {
-    uint64_t t = (uint64_t)acc | ((uint64_t)bytes << (8 * k));
-    k += cnt;
-    if (k >= 4) {
-      *p++ = (uint32_t)t;
-      t >>= 32;
-      k -= 4;
-    }
-    acc = (uint32_t)t;
+// Input: either the tile's bytes staged in LDS as big-endian dwords (ibe,
+// byte index of a = a - ibase), or src in global memory.  The bit position
+// is the only loop state: every step reads the 32-bit window at it (two
+// dwords + one 64-bit funnel shift) and looks up the 12-bit / 2-symbol
+// table.  While >= 30 bits remain no code can run past the string end, so
+// the main loop carries no end checks; the last < 30 bits go through a
+// checked tail loop.  Window bits past the end are don't-care: a code is
+// taken only if it ends at or before the end.
+template <bool LDSIN>
+__device__ __forceinline__ uint32_t window_at(const uint32_t *ibe, const uint32_t *gw,
+                                              uint32_t bp) {
+  const uint32_t wi = bp >> 5;
+  uint32_t w0, w1;
+  if (LDSIN) {
+    w0 = ibe[wi];
+    w1 = ibe[wi + 1];
+  } else {
+    w0 = __builtin_bswap32(gw[wi]);
+    w1 = __builtin_bswap32(gw[wi + 1]);
   }
-  __device__ __forceinline__ void finish() {
-    if (k) *p = acc;
-  }
-};
+  return (uint32_t)((((uint64_t)w0 << 32) | w1) >> (32u - (bp & 31u)));
+}
 
-// Decode one string [a, b) into sink.  Returns status; *fs / *fl receive the
-// final reference decode context (lib/nghttp2_hd_huffman.h:56-60).
-template <class Sink>
+// Code longer than the lookup: canonical length by binary search over the
+// left-justified limits, then the symbol.  Returns a lookup-style entry
+// (cnt 1, used = L), or ~0u when EOS (symbol 256) completes within `rem`.
+__device__ __forceinline__ uint32_t long_entry(const DecTables &T, uint32_t win, uint32_t rem) {
+  uint32_t lo = 0, hi = NLONG - 1;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (lo < hi) {
+      if (win < T.long_lim[mid]) hi = mid; else lo = mid + 1;
+    }
+  }
+  const uint32_t L = T.long_len[lo];
+  uint32_t sym = 0;
+  if (L <= rem) {
+    sym = T.canon[(win >> (32 - L)) + T.long_delta[lo]];
+    if (sym == 256) return 0xFFFFFFFFu;
+  }
+  return sym | (L << 16) | (1u << 25) | (L << 27);
+}
+
+template <bool LDSIN, class Sink>
 __device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t *__restrict__ src,
+                                              const uint32_t *ibe, uint32_t ibase,
                                               uint32_t a, uint32_t b, Sink &sink,
                                               uint32_t *fs, uint32_t *fl) {
-  uint64_t bb = 0;   // MSB-aligned bit buffer
-  uint32_t nb = 0;   // valid bits in bb
-  uint32_t pos = a;  // next byte to load
-  uint32_t rem = 8u * (b - a);  // bits of the string not yet decoded
+  const uint32_t *gw = nullptr;
+  uint32_t bp;  // bit position (LDS: from the staging base; global: from a & ~3)
+  if (LDSIN) {
+    bp = 8u * (a - ibase);
+  } else {
+    gw = reinterpret_cast<const uint32_t *>(src + (a & ~3u));
+    bp = 8u * (a & 3u);
+  }
+  const uint32_t bend = bp + 8u * (b - a);
   uint32_t nsym = 0;
+  uint32_t win = 0;
   bool failed = false;
-  while (rem) {
-    if (nb <= 32 && pos < b) {
-      const uint32_t x = load_be32(src, pos, b);
-      const uint32_t v = min(4u, b - pos);
-      bb |= (uint64_t)x << (32 - nb);
-      nb += 8 * v;
-      pos += v;
-    }
-    uint32_t e = T.lut[(uint32_t)(bb >> (64 - HD_HUFF_LUT_BITS))];
+  if (HD_DIAG_SKIP_LOOP) bp = bend;
+  // main loop: >= 30 bits left, no end checks
+  while (bend - bp >= 30u) {
+    win = window_at<LDSIN>(ibe, gw, bp);
+    uint32_t e = T.lut[win >> (32 - HD_HUFF_LUT_BITS)];
     if ((e & 0xF0000u) == 0) {
-      // code longer than the lookup (rare): canonical length by binary
-      // search over the left-justified limits, then the symbol
-      const uint32_t win = (uint32_t)(bb >> 32);
-      uint32_t lo = 0, hi = NLONG - 1;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (lo < hi) {
-          if (win < T.long_lim[mid]) hi = mid; else lo = mid + 1;
-        }
+      e = long_entry(T, win, 30u);
+      if (e == 0xFFFFFFFFu) {  // EOS decoded: the FSM's sticky failure state
+        failed = true;
+        break;
       }
-      const uint32_t L = T.long_len[lo];
-      uint32_t sym = 0;
-      if (L <= rem) {
-        sym = T.canon[(win >> (32 - L)) + T.long_delta[lo]];
-        if (sym == 256) {  // EOS decoded: the FSM's sticky failure state
-          failed = true;
-          break;
-        }
+    }
+    const uint32_t cnt = (e >> 25) & 3u;
+    sink.put2(e, cnt);
+    nsym += cnt;
+    bp += e >> 27;
+  }
+  // tail: < 30 bits left, every code checked against the end
+  uint32_t rem = bend - bp;
+  while (!failed && rem) {
+    win = window_at<LDSIN>(ibe, gw, bp);
+    uint32_t e = T.lut[win >> (32 - HD_HUFF_LUT_BITS)];
+    if ((e & 0xF0000u) == 0) {
+      e = long_entry(T, win, rem);
+      if (e == 0xFFFFFFFFu) {
+        failed = true;
+        break;
       }
-      e = sym | (L << 16);  // L up to 30: bits 16..20
     }
     const uint32_t L1 = (e >> 16) & 31u;
     const uint32_t L2 = (e >> 21) & 15u;
-    const bool ok1 = L1 <= rem;
-    const bool ok2 = ok1 && L2 != 0 && L1 + L2 <= rem;
-    const uint32_t cnt = (uint32_t)ok1 + (uint32_t)ok2;
-    sink.emit(ok1 ? (e & (ok2 ? 0xFFFFu : 0xFFu)) : 0u, cnt, nsym);
-    const uint32_t used = ok1 ? (ok2 ? L1 + L2 : L1) : 0u;
+    if (L1 > rem) break;  // the tail is a proper prefix of a code
+    const bool two = L2 != 0 && L1 + L2 <= rem;
+    const uint32_t cnt = two ? 2u : 1u;
+    sink.put2(e, cnt);
     nsym += cnt;
-    bb <<= used;
-    nb -= used;
+    const uint32_t used = two ? L1 + L2 : L1;
+    bp += used;
     rem -= used;
-    if (!ok1) break;
   }
   sink.finish();
   if (failed) {
@@ -486,9 +548,10 @@ __device__ __forceinline__ int32_t decode_one(const DecTables &T, const uint8_t 
     return sink.ovf ? NGHTTP2_AMD_ERR_BUFFER_ERROR : NGHTTP2_AMD_ERR_HEADER_COMP;
   }
   // tail = the last `rem` (< 30) bits: a proper prefix of a code, i.e. an
-  // internal node of the code tree -> the FSM state it leaves behind.
+  // internal node of the code tree -> the FSM state it leaves behind.  When
+  // rem > 0 the loop left right after reading the window at bp.
   const uint32_t t = rem;
-  const uint32_t v = t ? (uint32_t)(bb >> (64 - t)) : 0u;
+  const uint32_t v = t ? (win >> (32 - t)) : 0u;
   const bool accept = (t <= 7) && (v == (1u << t) - 1u);
   *fs = t ? T.depth_ids[T.depth_base[t] + (v - T.depth_lo[t])] : 0u;
   *fl = (accept ? HUFF_ACCEPTED : 0u) | ((t < 4 && nsym) ? HUFF_SYM : 0u);
@@ -543,6 +606,7 @@ __global__ __launch_bounds__(DEC_WG) void k_decode(const uint8_t *__restrict__ s
                                                    uint8_t *__restrict__ flags_out) {
   __shared__ DecTables T;
   __shared__ uint32_t obuf[AUTO ? DEC_OBUF / 4 : 1];
+  __shared__ uint4 ibuf[DEC_IBUF / 16 + 1];
   __shared__ uint32_t hist[256];
   __shared__ uint16_t perm[DEC_WG];
   __shared__ uint32_t red[DEC_WG / 64];
@@ -552,31 +616,49 @@ __global__ __launch_bounds__(DEC_WG) void k_decode(const uint8_t *__restrict__ s
     const uint32_t mine = t0 + threadIdx.x;
     const bool live0 = mine < n;
     const uint32_t len0 = live0 ? off[mine + 1] - off[mine] : 0u;
-    const uint32_t r = sorted_lane<DEC_WG>(len0, live0, hist, perm, red);
+    const uint32_t r = HD_DEC_SORT ? sorted_lane<DEC_WG>(len0, live0, hist, perm, red)
+                                   : (live0 ? threadIdx.x : 0xFFFFFFFFu);
     const uint32_t s = t0 + r;
     const bool live = r != 0xFFFFFFFFu;
     uint32_t fs = 0, fl = 0;
     int32_t st = 0;
+    // stage the tile's input bytes in LDS with one bulk coalesced load
+    const uint32_t s1 = min(t0 + DEC_WG, n);
+    const uint32_t ibase = off[t0] & ~15u;
+    const uint32_t nchunk = (off[s1] - ibase + 15u) >> 4;
+    const bool in_lds = HD_DEC_INSTAGE && nchunk <= DEC_IBUF / 16;  // uniform
+    if (in_lds) {  // big-endian dwords: the decoder's windows need no swaps
+      const uint4 *g = reinterpret_cast<const uint4 *>(src + ibase);
+      for (uint32_t i = threadIdx.x; i < nchunk; i += DEC_WG) {
+        const uint4 v = g[i];
+        ibuf[i] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
+                             __builtin_bswap32(v.z), __builtin_bswap32(v.w));
+      }
+      if (threadIdx.x == 0) ibuf[nchunk] = make_uint4(0, 0, 0, 0);
+      __syncthreads();
+    }
+    const uint32_t *ib = in_lds ? reinterpret_cast<const uint32_t *>(ibuf) : nullptr;
     if (AUTO) {
-      const uint32_t s1 = min(t0 + DEC_WG, n);
       const uint64_t lo = auto_slot(off[t0] - off0, t0);
       const uint64_t hi = auto_slot(off[s1] - off0, s1);
-      const bool staged = (hi - lo) <= DEC_OBUF && hi <= dst_cap;  // uniform
+      const bool staged = HD_DEC_OUTSTAGE && (hi - lo) <= DEC_OBUF && hi <= dst_cap;  // uniform
       if (live) {
         const uint32_t a = off[s], b = off[s + 1];
         const uint64_t o64 = auto_slot(a - off0, s);
         dst_off[s] = (uint32_t)o64;
         if (s == n - 1) dst_off[n] = (uint32_t)auto_slot(b - off0, n);
         if (staged) {
-          WordSink<lds_u32 *> sink;
-          sink.init((lds_u32 *)obuf + ((o64 - lo) >> 2));
-          st = decode_one(T, src, a, b, sink, &fs, &fl);
+          SlotSink<lds_u8 *> sink;
+          sink.init((lds_u8 *)obuf + (o64 - lo));
+          st = ib ? decode_one<true>(T, src, ib, ibase, a, b, sink, &fs, &fl)
+                  : decode_one<false>(T, src, ib, ibase, a, b, sink, &fs, &fl);
         } else if (auto_slot(b - off0, s + 1) > dst_cap) {
           st = NGHTTP2_AMD_ERR_BUFFER_ERROR;
         } else {
-          WordSink<uint32_t *> sink;
-          sink.init(reinterpret_cast<uint32_t *>(dst + o64));
-          st = decode_one(T, src, a, b, sink, &fs, &fl);
+          SlotSink<uint8_t *> sink;
+          sink.init(dst + o64);
+          st = ib ? decode_one<true>(T, src, ib, ibase, a, b, sink, &fs, &fl)
+                  : decode_one<false>(T, src, ib, ibase, a, b, sink, &fs, &fl);
         }
       }
       if (staged) {
@@ -588,9 +670,10 @@ __global__ __launch_bounds__(DEC_WG) void k_decode(const uint8_t *__restrict__ s
     } else if (live) {
       const uint32_t a = off[s], b = off[s + 1];
       const uint32_t o = dst_off[s];
-      ByteSink sink;
+      CheckedSink sink;
       sink.init(dst + o, dst_off[s + 1] - o);
-      st = decode_one(T, src, a, b, sink, &fs, &fl);
+      st = ib ? decode_one<true>(T, src, ib, ibase, a, b, sink, &fs, &fl)
+                : decode_one<false>(T, src, ib, ibase, a, b, sink, &fs, &fl);
     }
     if (live) {
       status[s] = st;

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Time ablation variants of the decode kernel (and encode) in ONE process,
+interleaved rounds (cdna_hip_programming.md 5.4 rule 24)."""
+import ctypes, glob, json, os, sys
+import numpy as np
+import torch
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+from nghttp2_amd import workloads as W
+import nghttp2_amd
+
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+dev = torch.device("cuda:0")
+pool, off = W.gen_pseudo_headers(1 << 20) if cfg == 2 else W.gen_mixed_values(1 << 20)
+codec = nghttp2_amd.HuffmanBatchCodec(dev)
+src = torch.from_numpy(pool).to(dev)
+so = torch.from_numpy(off.view(np.int32)).to(dev)
+enc, eo = codec.encode(src, so, raw_bytes=int(off[-1]))
+torch.cuda.synchronize()
+E = int(eo[-1].item())
+n = len(off) - 1
+dcap = codec.decode_bound(E, n)
+dst = torch.empty(dcap, dtype=torch.uint8, device=dev)
+doff = torch.empty(n + 1, dtype=torch.int32, device=dev)
+st = torch.empty(n, dtype=torch.int32, device=dev)
+libs = {}
+for p in sorted(glob.glob(os.path.join(HERE, "lib_*.so"))):
+    L = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+    vp = ctypes.c_void_p
+    L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]
+    libs[os.path.basename(p)[4:-3]] = L
+s = torch.cuda.current_stream()
+def run(L):
+    L.nghttp2_amd_hd_huff_decode_batch_auto(ctypes.c_void_p(enc.data_ptr()), ctypes.c_void_p(eo.data_ptr()), n,
+        ctypes.c_void_p(dst.data_ptr()), dcap, ctypes.c_void_p(doff.data_ptr()), ctypes.c_void_p(st.data_ptr()),
+        None, None, ctypes.c_void_p(s.cuda_stream))
+res = {k: [] for k in libs}
+for k, L in libs.items():
+    for _ in range(3): run(L)
+torch.cuda.synchronize()
+for rnd in range(10):
+    for k, L in libs.items():
+        a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+        a.record(s); run(L); b.record(s); torch.cuda.synchronize()
+        res[k].append(a.elapsed_time(b) * 1000)
+out = {k: {"median_us": round(float(np.median(v)), 1), "min_us": round(float(np.min(v)), 1)} for k, v in res.items()}
+print(json.dumps({"config": cfg, "decode_variants": out}, indent=1))
