@@ -30,6 +30,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CONFIG_NAMES = {
     2: "1M short pseudo-header strings (8-64 B), encode+decode, 1xMI355X",
     3: "1M mixed-length header values (16-1024 B, Zipf), encode+decode, 1xMI355X",
+    4: "16M mixed-length header strings (16-1024 B, Zipf) sharded by bytes across the GPUs "
+       "(no collective), encode+decode",
 }
 
 
@@ -38,8 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3])
-    ap.add_argument("--strings", type=int, default=1 << 20)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--strings", type=int, default=None,
+                    help="strings per GPU (configs 2/3) or in total (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-resident", action="store_true",
@@ -90,12 +93,24 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    n = args.strings
     seed = W.SEED[args.config] + 7919 * rank  # each rank its own batch (weak scaling)
+    scaling = "weak"
     if args.config == 2:
+        n = args.strings or (1 << 20)
         pool, off = W.gen_pseudo_headers(n, seed=seed)
-    else:
+    elif args.config == 3:
+        n = args.strings or (1 << 20)
         pool, off = W.gen_mixed_values(n, seed=seed)
+    else:  # one fixed set, byte-balanced contiguous shard per rank (strong)
+        from nghttp2_amd import shard as S
+        n_total = args.strings or (1 << 24)
+        lengths = W.mixed_lengths(n_total)
+        all_off = np.zeros(n_total + 1, dtype=np.int64)
+        np.cumsum(lengths, out=all_off[1:])
+        s0, s1 = S.byte_balanced_bounds(all_off, world)[rank]
+        pool, off = W.gen_mixed_range(lengths, s0, s1)
+        n = s1 - s0
+        scaling = "strong"
     raw_bytes = int(off[-1])
 
     codec = nghttp2_amd.HuffmanBatchCodec(dev)
@@ -183,14 +198,56 @@ def main():
            "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-           "data": "synthetic (numpy PCG64, seed 0x%X + 7919*rank)" % W.SEED[args.config],
+           "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+           "data": ("synthetic (numpy PCG64, seed 0x%X + 7919*rank)" % W.SEED[args.config])
+                   if args.config != 4 else "synthetic (numpy PCG64, chunk-seeded 0x%X)" % W.SEED[4],
            "config": {"workload": CONFIG_NAMES[args.config], "strings_per_gpu": n,
                       "raw_bytes_per_gpu": raw_bytes, "enc_bytes_per_gpu": enc_total,
                       "E_over_R": round(enc_total / raw_bytes, 4),
                       "alg_bytes_per_step_all_gpus": int(B_total),
                       "parallelism": "shard%d (independent batches, no collective)" % world},
            "roofline": roof}
+
+    if args.host_resident:
+        # The path as deployed: raw headers start in (pinned) host memory and
+        # both results go back to it -- H2D raw pool + offsets, encode,
+        # decode, D2H encoded pool + offsets and decoded slots + status, all
+        # async on the one stream.  Same B accounting as `value`.
+        h_src = torch.from_numpy(pool).pin_memory()
+        h_off = torch.from_numpy(off.view(np.int32)).pin_memory()
+        h_enc = torch.empty(enc_total + 16, dtype=torch.uint8).pin_memory()
+        h_eoff = torch.empty(n + 1, dtype=torch.int32).pin_memory()
+        dec_used = int(dec_off[-1].item())
+        h_dec = torch.empty(dec_used, dtype=torch.uint8).pin_memory()
+        h_st = torch.empty(n, dtype=torch.int32).pin_memory()
+
+        def host_step():
+            src.copy_(h_src, non_blocking=True)
+            src_off.copy_(h_off, non_blocking=True)
+            step()
+            h_enc[:enc_total].copy_(enc[:enc_total], non_blocking=True)
+            h_eoff.copy_(enc_off, non_blocking=True)
+            h_dec.copy_(dec[:dec_used], non_blocking=True)
+            h_st.copy_(status, non_blocking=True)
+
+        for _ in range(max(1, args.warmup)):
+            host_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        th0 = time.perf_counter()
+        for _ in range(args.steps):
+            host_step()
+        torch.cuda.synchronize()
+        th = time.perf_counter() - th0
+        assert np.array_equal(h_st.numpy(), raw_len)
+        pcie = (raw_bytes + 4 * (n + 1)) + (enc_total + 4 * (n + 1)) + dec_used + 4 * n
+        out["host_resident"] = {
+            "value": round(B_rank * args.steps / th / 1e9, 3), "unit": "GB/s",
+            "ms_per_step": round(th / args.steps * 1e3, 4),
+            "pcie_bytes_per_step": pcie,
+            "note": "pinned H2D raw+offsets, encode, decode, D2H encoded+offsets, "
+                    "decoded slots+status; same algorithmic-B accounting as value"}
 
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         threads = max(1, min(args.cpu_threads, cpu_cores_available()))

@@ -34,6 +34,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifndef NGHTTP2_AMD_EXTERN
+#define NGHTTP2_AMD_EXTERN __attribute__((visibility("default")))
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -52,7 +56,7 @@ extern "C" {
 #define NGHTTP2_AMD_HUFF_FAIL_STATE 0x100u
 
 /* Library version string, e.g. "nghttp2_amd_hd 0.1.0 gfx950". */
-const char *nghttp2_amd_hd_version(void);
+NGHTTP2_AMD_EXTERN const char *nghttp2_amd_hd_version(void);
 
 /* Copies the engine's Huffman tables out in the reference's struct layouts
  * so a caller can check them against lib/nghttp2_hd_huffman_data.c without a
@@ -60,7 +64,7 @@ const char *nghttp2_amd_hd_version(void);
  * bytes, lib/nghttp2_hd_huffman_data.c:29-94), dec_out receives
  * huff_decode_table (257 x 16 x {u16 fstate, u8 flags, u8 sym} = 16448 bytes,
  * :96-4980).  Either pointer may be NULL.  Returns 0. */
-int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out);
 
 /* ------------------------------------------------------------------ */
 /* Sizing helpers (host-only, no GPU needed)                           */
@@ -69,16 +73,16 @@ int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out);
 /* Upper bound of the encoded pool for `raw_bytes` bytes in `n` strings:
  * every symbol is at most 30 bits (RFC 7541 App. B), plus one padding byte
  * per string, rounded up to 16. */
-size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_bound(uint64_t raw_bytes, uint32_t n);
 
 /* Size of the decode output pool nghttp2_amd_hd_huff_decode_batch_auto needs
  * for an encoded pool of `enc_bytes` bytes in `n` strings:
  * floor(8 * enc_bytes / 5) + 4 * n, rounded up. */
-size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n);
 
 /* Bytes of device workspace nghttp2_amd_hd_huff_encode_batch and
  * nghttp2_amd_hd_huff_decode_slots need for `n` strings. */
-size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
 
 /* ------------------------------------------------------------------ */
 /* Batched device-resident API                                          */
@@ -101,7 +105,7 @@ size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
  * capacity returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT (the kernels never
  * write past dst_cap).
  */
-int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst, size_t dst_cap,
                                      uint32_t *dst_off, void *workspace,
                                      size_t workspace_size, void *stream);
@@ -110,7 +114,7 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
  * Encoded lengths only: enc_len[i] = nghttp2_hd_huff_encode_count(string i)
  * (lib/nghttp2_hd_huffman.c:34-43).
  */
-int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src,
                                            const uint32_t *src_off, uint32_t n,
                                            uint32_t *enc_len, void *stream);
 
@@ -121,7 +125,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src,
  * used at lib/nghttp2_hd.c:2080-2082 / :2166-2168).  dst_off[n] is the
  * pool size to allocate.
  */
-int nghttp2_amd_hd_huff_decode_slots(const uint32_t *src_off, uint32_t n,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_slots(const uint32_t *src_off, uint32_t n,
                                      uint32_t *dst_off, void *workspace,
                                      size_t workspace_size, void *stream);
 
@@ -149,7 +153,7 @@ int nghttp2_amd_hd_huff_decode_slots(const uint32_t *src_off, uint32_t n,
  * On -523 the bytes decoded before the failure are still written (as the
  * reference leaves them in buf), so dst matches the reference byte for byte.
  */
-int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst,
                                      const uint32_t *dst_off, int32_t *status,
                                      uint16_t *fstate, uint8_t *flags,
@@ -165,7 +169,7 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
  * hold nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes; strings whose slot
  * would end past dst_cap get -502 and write nothing.
  */
-int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint8_t *dst, size_t dst_cap,
                                           uint32_t *dst_off, int32_t *status,
                                           uint16_t *fstate, uint8_t *flags, void *stream);
@@ -181,7 +185,7 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
  * the number of bytes written (the reference returns srclen then; the
  * caller checks fstate == 0x100 for failure_state, :145-147).
  */
-int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src_off,
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, const uint32_t *src_off,
                                          uint32_t n, uint8_t *dst, const uint32_t *dst_off,
                                          int32_t *status, uint16_t *fstate, uint8_t *flags,
                                          const uint16_t *init_fstate,

@@ -737,7 +737,6 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
 // C ABI
 // ---------------------------------------------------------------------------
 static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
-static inline uint32_t ntiles_dec(uint32_t n) { return (n + DEC_WG - 1) / DEC_WG; }
 // Persistent grids are sized to what is resident at once (occupancy query
 // x CU count, cached per kernel), so no workgroup runs as a second "wave"
 // and the LDS tables are staged once per resident workgroup.

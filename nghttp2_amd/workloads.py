@@ -72,6 +72,36 @@ def gen_mixed_values(n, seed=SEED[3], lo=16, hi=1024):
     return _pool_from_lengths(lengths, chars)
 
 
+CHUNK = 1 << 16  # strings per independently seeded generation chunk
+
+
+def mixed_lengths(n, seed=SEED[4], lo=16, hi=1024):
+    """Config-4 lengths for all n strings (cheap), chunk-seeded."""
+    out = np.empty(n, dtype=np.int64)
+    for c0 in range(0, n, CHUNK):
+        rng = np.random.Generator(np.random.PCG64([seed, c0 // CHUNK]))
+        out[c0:c0 + CHUNK] = zipf_lengths(rng, min(CHUNK, n - c0), lo, hi)
+    return out
+
+
+def gen_mixed_range(lengths, s0, s1, seed=SEED[4]):
+    """Characters of strings [s0, s1) of a chunk-seeded config-4 set: each
+    rank generates only its own shard.  Returns (pool, off) rebased to 0."""
+    parts = []
+    for c in range(s0 // CHUNK, (max(s1, s0 + 1) - 1) // CHUNK + 1):
+        c0, c1 = c * CHUNK, min((c + 1) * CHUNK, len(lengths))
+        rng = np.random.Generator(np.random.PCG64([seed, 1 << 20, c]))
+        tot = int(lengths[c0:c1].sum())
+        cookie = rng.choice(COOKIE_ALPHABET, size=tot)
+        other = rng.choice(PRINTABLE, size=tot)
+        chars = np.where(rng.random(tot) < 0.85, cookie, other).astype(np.uint8)
+        cum = np.concatenate([[0], np.cumsum(lengths[c0:c1])])
+        a, b = max(s0, c0) - c0, min(s1, c1) - c0
+        parts.append(chars[cum[a]:cum[b]])
+    chars = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return _pool_from_lengths(lengths[s0:s1], chars)
+
+
 def gen_all_bytes(n, seed=1, lo=0, hi=64):
     """Uniformly random bytes 0..255 (exercises every code length)."""
     rng = np.random.Generator(np.random.PCG64(seed))
