@@ -167,9 +167,11 @@ def build():
     # 12-bit multi-symbol lookup table for the canonical decoder: for every
     # 12-bit window, the first code if it is <= 12 bits (sym1, L1) and, when
     # the rest of the window holds another whole code, the second (sym2, L2).
-    # Entry: sym1 | sym2 << 8 | L1 << 16 | L2 << 21 | cnt << 25 | (L1+L2) << 27;
-    # cnt = symbols in the entry (1 or 2); L1 == 0 means the first
-    # code is longer than 12 bits (all such codes start with >= 10 ones).
+    # Entry: sym1 | L1 << 8 | L2 << 13 | sym2 << 16 | cnt << 24 | (L1+L2) << 27;
+    # cnt = symbols in the entry (1 or 2; L2 <= 12 - 5 fits 3 bits).  A zero
+    # entry means the first code is longer than 12 bits (all such codes start
+    # with >= 10 ones).  sym2 sits in bits 16..23 so that a byte store of the
+    # high half (ds_write_b8_d16_hi) emits it without a shift.
     lut = []
     for w in range(1 << LUT_BITS):
         def first_code(v, nbits):
@@ -184,9 +186,10 @@ def build():
             assert s1 != EOS
             r = LUT_BITS - L1
             s2, L2 = first_code(w & ((1 << r) - 1), r) if r else (None, 0)
-            e = s1 | (L1 << 16) | (1 << 25) | (L1 << 27)
+            e = s1 | (L1 << 8) | (1 << 24) | (L1 << 27)
             if s2 is not None:
-                e = s1 | (s2 << 8) | (L1 << 16) | (L2 << 21) | (2 << 25) | ((L1 + L2) << 27)
+                assert L2 <= 7
+                e = s1 | (L1 << 8) | (L2 << 13) | (s2 << 16) | (2 << 24) | ((L1 + L2) << 27)
         lut.append(e)
     # long codes: (L, left-justified exclusive limit as a 32-bit-window
     # compare, first code, canonical index base) for every length > LUT_BITS
@@ -254,7 +257,7 @@ def write_inc(t, path):
     for i in range(0, 256, 16):
         w("  " + ", ".join("%d" % v for v in t["id_list"][i:i + 16]) + ",")
     w("};")
-    w("/* canonical decoder: %d-bit lookup, sym1 | sym2 << 8 | L1 << 16 | L2 << 21 | cnt << 25 | used << 27 */" % LUT_BITS)
+    w("/* canonical decoder: %d-bit lookup, sym1 | L1 << 8 | L2 << 13 | sym2 << 16 | cnt << 24 | used << 27 */" % LUT_BITS)
     w("#define HD_HUFF_LUT_BITS %d" % LUT_BITS)
     w("HD_TBL const unsigned int hd_huff_lut[%d] = {" % (1 << LUT_BITS))
     for i in range(0, 1 << LUT_BITS, 8):

@@ -4,11 +4,10 @@
 set -e
 HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../../nghttp2_amd/csrc/hd_huff.hip
+rm -f $HERE/lib_*.so
 build() { name=$1; shift; (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 "$@" -o $HERE/lib_$name.so $SRC); echo built $name; }
 build base
-build noinstage -DHD_DEC_INSTAGE=0
-build nosort -DHD_DEC_SORT=0
 build nooutstage -DHD_DEC_OUTSTAGE=0
-build noinstage_nosort -DHD_DEC_INSTAGE=0 -DHD_DEC_SORT=0
-build skiploop -DHD_DIAG_SKIP_LOOP=1
-build skiploop_noinstage -DHD_DIAG_SKIP_LOOP=1 -DHD_DEC_INSTAGE=0
+build window -DHD_BITBUF=0
+build win_noout -DHD_BITBUF=0 -DHD_DEC_OUTSTAGE=0
+build stamps -DHD_DIAG_STAMPS=1
