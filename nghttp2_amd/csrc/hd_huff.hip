@@ -48,34 +48,37 @@ namespace host {
 #define ENC_OBUF 16384  // LDS output staging per encode workgroup (bytes)
 
 // Ablation switch (tools/diag builds variants; the product uses the default)
-#ifndef HD_DEC_OUTSTAGE
-#define HD_DEC_OUTSTAGE 1  // stage the decode tile's output slots in LDS
-#endif
 
 #ifndef HD_BITBUF
-#define HD_BITBUF 1  // fast loop: register bit buffer (1 LDS round trip per step)
+#define HD_BITBUF 0  // fast loop: 1 = register bit buffer; 0 = LDS window per step (fewer VALU; faster at high occupancy)
 #endif
 #ifndef HD_DIAG_STAMPS
 #define HD_DIAG_STAMPS 0   // diagnostic build only: per-phase s_memtime sums
 #endif
 #if HD_DIAG_STAMPS
-// [wg][slot]: 0 setup, 1 sort, 2 pass1, 3 verify, 4 scan, 5 pass2, 6 report,
-// 7 copy, 8 verify iterations, 9 mismatches, 10 rounds, 11 tiles
+// [wg][slot]: per-phase cycles (slots 0..7, accumulated in registers of
+// thread 0 and stored once), 8 verify iterations, 9 mismatches, 10 rounds,
+// 11 tiles, 12..14 wave loop trips (fast, checked, warm-up)
 __device__ unsigned long long g_stamps[4096][16];
 #define STAMP(slot, t0)                                                        \
   do {                                                                         \
     __syncthreads();                                                           \
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime();               \
-    if (threadIdx.x == 0) g_stamps[blockIdx.x & 4095][slot] += t1_ - (t0);     \
+    stamp_acc[slot] += t1_ - (t0);                                             \
     (t0) = t1_;                                                                \
   } while (0)
-#define COUNT(slot, v) do { if (threadIdx.x == 0) g_stamps[blockIdx.x & 4095][slot] += (v); } while (0)
-__device__ uint32_t g_dctr[3];  // per-thread loop trips: fast, checked, warm-up (diag)
+#define COUNT(slot, v) do { if (threadIdx.x == 0) stamp_acc[slot] += (v); } while (0)
+#define STAMP_FLUSH()                                                          \
+  do {                                                                         \
+    if (threadIdx.x == 0)                                                      \
+      for (int s_ = 0; s_ < 12; ++s_) g_stamps[blockIdx.x & 4095][s_] += stamp_acc[s_]; \
+  } while (0)
 #define DCTR(k) (++dctr[k])
 #else
-#define DCTR(k) do { } while (0)
 #define STAMP(slot, t0) do { } while (0)
 #define COUNT(slot, v) do { } while (0)
+#define STAMP_FLUSH() do { } while (0)
+#define DCTR(k) do { } while (0)
 #endif
 
 #define HUFF_ACCEPTED 0x01u
@@ -390,6 +393,7 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
 #define NLONG_PAD 16  // search width (padding rows repeat the last row)
 struct DecTables {
   uint32_t lut[1 << HD_HUFF_LUT_BITS];
+  uint32_t lut2[64];               // 13..16-bit codes (second level)
   uint32_t long_lim[NLONG_PAD];    // exclusive left-justified limit (last: ~0)
   uint32_t long_delta[NLONG_PAD];  // canonical base - first code (mod 2^32)
   uint32_t long_len[NLONG_PAD];
@@ -402,6 +406,7 @@ struct DecTables {
 __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads) {
   const uint32_t t = threadIdx.x;
   for (uint32_t i = t; i < (1u << HD_HUFF_LUT_BITS); i += nthreads) T.lut[i] = dev::hd_huff_lut[i];
+  if (t < 64) T.lut2[t] = dev::hd_huff_lut2[t];
   for (uint32_t i = t; i < 257; i += nthreads) T.canon[i] = dev::hd_huff_canon_sym[i];
   if (t < 30) {
     T.depth_lo[t] = dev::hd_huff_depth_lo[t];
@@ -427,31 +432,30 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
 }
 
 // ---------------------------------------------------------------------------
-// Item decoding (DESIGN.md "decode").  A tile is DEC_NS consecutive strings.
-// A string of E encoded bytes is cut into m = max(1, ceil(E / 64)) ITEMS:
+// Item decoding (DESIGN.md "decode").  A string of E encoded bytes is cut
+// into m = max(1, ceil(E / 64)) ITEMS:
 //   item (i, 0)   the string from its first bit (exact), up to the first
 //                 codeword boundary at or after byte sa[i] + 64, or its end;
 //   item (i, k>0) the piece from byte sa[i] + 64 k: a speculative entry
 //                 (warm-up from SUB_OV bytes early to the first boundary >=
 //                 the piece start), then on to the first boundary >= piece
 //                 start + 64, or the string end.
-// Rounds take DEC_NT consecutive items; their input bytes are contiguous
-// (<= 64 DEC_NT + warm-up) and are staged once in LDS (coalesced 16-byte
-// loads, byte-swapped to big-endian words).  Lanes are assigned items sorted
-// by length, so a wave's lanes finish together.  An item's entry is verified
-// against the previous item's exit (or the carry from the previous round);
-// mismatches are re-decoded from the settled exit, which makes the result
-// exact for any input.  k = 0 items write in pass 1; k > 0 items write in
-// pass 2 at their string's running symbol count (a segmented scan).  Output
-// goes into an LDS image of the round's slot range and is stored with
-// coalesced 16-byte writes.
+// A wave takes 64 consecutive items per round (one per lane); their input
+// bytes are contiguous (<= 64 * 64 + warm-up) and are staged once in the
+// wave's LDS region (coalesced 16-byte loads, byte-swapped to big-endian
+// words).  An item's entry is verified against the previous lane's exit (or
+// the carry from the previous round); mismatches are re-decoded from the
+// settled exit, which makes the result exact for any input.  k = 0 items
+// write in pass 1; k > 0 items write in pass 2 at their string's running
+// symbol count (a segmented scan across lanes).
 // ---------------------------------------------------------------------------
-#define DEC_NT 256                                 // lanes per decode workgroup
-#define DEC_NS 512                                 // strings per decode tile
+#define WAVE 64
+#define DEC_WAVES 8                                // waves per decode workgroup (one table copy)
+#define DEC_NT (WAVE * DEC_WAVES)
+#define TASK_STR 64                                // strings per wave task
 #define PIECE_BYTES 64u                            // input bytes per item (string piece)
 #define SUB_OV 16u                                 // warm-up bytes of a k > 0 piece
-#define IBUF_BYTES (PIECE_BYTES * DEC_NT + 96u)    // + warm-up, alignment, overrun, read-ahead
-#define DEC_OBUF 30720u                            // LDS output image per round (>= 8/5 IBUF + 4 DEC_NT)
+#define IBUF_W (PIECE_BYTES * WAVE + 96u)          // per-wave staged input (+ warm-up, alignment, reach)
 #define XFAIL 0xFFFFFFFFu    // exit after EOS (sticky failure)
 #define XUNKNOWN 0xFFFFFFFEu // speculative entry lost (EOS during warm-up)
 #define NOSPEC 0xFFFFFFFDu   // lane has no speculative item
@@ -473,25 +477,10 @@ __device__ __forceinline__ uint32_t win_q(const lds_u32 *ibe, uint32_t q) {  // 
 __device__ __forceinline__ uint32_t win_at(const lds_u32 *ibe, uint32_t bp) { return win_q(ibe, bp - 1u); }
 
 // Decode output sinks.  put2(e, cnt) appends the cnt (1..2) symbols of a
-// table entry: sym1 in bits 0..7, sym2 in bits 16..23.
-//  LdsFast   second byte stored unconditionally: only for items whose
-//            following byte is this lane's own next store, slot slack, or a
-//            byte that a later phase (after a barrier) rewrites -- pass 1.
-//  LdsSafe   second byte to a private junk dword when cnt == 1 -- pass 2,
-//            where the next byte belongs to a concurrently running lane.
-//  GlobalOut direct stores (round image too large to stage).
-template <bool SAFE>
-struct LdsSink {
-  lds_u8 *p, *junk;
-  __device__ __forceinline__ uint32_t count() const { return (uint32_t)(uintptr_t)p; }
-  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
-    p[0] = (uint8_t)e;
-    lds_u8 *q = p + 1;
-    if (SAFE) q = cnt > 1 ? q : junk;
-    q[0] = (uint8_t)(e >> 16);
-    p += cnt;
-  }
-};
+// table entry: sym1 in bits 0..7, sym2 in bits 16..23.  Output goes straight
+// to global memory: DwordSink for items that start an engine slot (dword
+// aligned), GlobalSink (bytes) for pieces that continue a string, whose
+// first byte shares a dword with the previous piece (another lane).
 struct GlobalSink {
   uint8_t *p;
   __device__ __forceinline__ uint32_t count() const { return (uint32_t)(uintptr_t)p; }
@@ -574,6 +563,12 @@ __device__ __forceinline__ uint32_t long_entry(const DecTables &T, uint32_t win,
   return (L <= rem ? sym : 0u) | (L << 8) | (1u << 24) | (L << 27);
 }
 
+// First-level miss: the 13..16-bit second level, else the search.
+__device__ __forceinline__ uint32_t slow_entry(const DecTables &T, uint32_t win, uint32_t rem) {
+  const uint32_t e = T.lut2[(win >> 16) & 63u];
+  return e ? e : long_entry(T, win, rem);
+}
+
 // Decode from bit bp (positions relative to the staged round) of a string
 // ending at bit bend.  SPEC: warm up to the first boundary >= bseg (the
 // entry).  Then decode, emitting into sink, to the first boundary >= bstop,
@@ -597,7 +592,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
       const uint32_t w = win_at(ibe, bp);
       const uint32_t rem = bend - bp;
       uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
-      if (e == 0u) e = long_entry(T, w, rem);
+      if (e == 0u) e = slow_entry(T, w, rem);
       if (e == 0xFFFFFFFFu) {
         r.entry = r.exit = XUNKNOWN;
         return r;
@@ -628,7 +623,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
       const uint32_t w = (uint32_t)(bb >> 32);
       uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
       if (e == 0u) {
-        e = long_entry(T, w, 30u);
+        e = slow_entry(T, w, 30u);
         if (e == 0xFFFFFFFFu) {
           F = INT32_MIN;
           e = 0u;
@@ -654,7 +649,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
     const uint32_t w = win_q(ibe, q);
     uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
     if (e == 0u) {
-      e = long_entry(T, w, 30u);
+      e = slow_entry(T, w, 30u);
       if (e == 0xFFFFFFFFu) {
         F = INT32_MIN;
         e = 0u;
@@ -674,7 +669,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
     const uint32_t w = win_at(ibe, bp);
     uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
     if (e == 0u) {
-      e = long_entry(T, w, rem);
+      e = slow_entry(T, w, rem);
       if (e == 0xFFFFFFFFu) {
         failed = true;
         break;
@@ -727,36 +722,25 @@ __device__ __host__ __forceinline__ uint64_t auto_slot(uint32_t x, uint32_t s) {
   return 4u * (((g + 3u) >> 2) + s);
 }
 
-// Tile string holding item q: the last i with sbase[i] <= q.
-__device__ __forceinline__ uint32_t find_string(const uint32_t *sbase, uint32_t nstr, uint32_t q) {
-  uint32_t lo = 0, hi = nstr - 1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (sbase[mid] <= q) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-struct DecShared {
-  uint32_t ibe[IBUF_BYTES / 4 + 4];  // 16 spare bytes, then the round's input (big-endian words)
-  DecTables T;
-  uint32_t sa[DEC_NS + 1];       // tile string offsets
-  uint32_t sbase[DEC_NS + 1];    // first item of each tile string
-  uint32_t es[DEC_NT], xs[DEC_NT], cs[DEC_NT];  // per item of the round: entry, exit, symbols
-  uint32_t seg[DEC_NT];          // symbols of the item's string through the item
-  uint32_t hist[128];
-  uint16_t perm[DEC_NT];
-  uint8_t head[DEC_NT];          // item is its string's first (k = 0)
-  uint8_t unsettled[DEC_NT];
-  uint32_t red[2 * (DEC_NT / 64)];
-  uint32_t qmax;                 // round: end of the output image (relative)
-  uint32_t rinfo[2];             // round: first input byte (incl. warm-up), string of the first item
-  uint32_t carry[2];             // {exit, symbols so far} of the string running into the next round
+// One lane's item within its wave's round (positions relative to the
+// wave's staged input).
+struct ItemPos {
+  uint32_t i, k;        // task string, piece
+  uint32_t a, b, s;     // string bytes [a, b), piece start s
+  bool last;            // the string's last piece
 };
 
-// One persistent workgroup per group of tiles.  AUTO: engine slots (written
-// to dst_off), staged in LDS per round when the round's slot range fits;
-// else caller slots written directly, capacity-checked.
+// Wave tasks: a wave owns TASK_STR consecutive strings at a time and runs
+// its own rounds of 64 items (one per lane) over them -- no workgroup
+// barriers, so staging, decoding and the bookkeeping of different waves
+// overlap freely.  Verify and the segmented scan are wave-level (shuffles).
+// AUTO: engine slots (written to dst_off); else caller slots,
+// capacity-checked.
+struct DecShared {
+  uint32_t ibe[DEC_WAVES][IBUF_W / 4 + 4];  // per wave: 16 spare bytes, then the round's input
+  DecTables T;
+};
+
 template <bool AUTO>
 __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ src,
                                                    const uint32_t *__restrict__ off, uint32_t n,
@@ -766,163 +750,112 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
                                                    uint16_t *__restrict__ fstate_out,
                                                    uint8_t *__restrict__ flags_out) {
   __shared__ DecShared S;
-  __shared__ uint32_t obuf[(AUTO && HD_DEC_OUTSTAGE) ? DEC_OBUF / 4 + 64 : 1];
-  const uint32_t tid = threadIdx.x;
-  const lds_u32 *ibe = (const lds_u32 *)S.ibe;
-  lds_u8 *junk = (lds_u8 *)(obuf + ((AUTO && HD_DEC_OUTSTAGE) ? DEC_OBUF / 4 : 0)) + 4u * (tid & 63u);
-  stage_dec_tables(S.T, DEC_NT);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lds_u32 *ibw = (lds_u32 *)S.ibe[wv];
+  const lds_u32 *ibe = ibw;
+  stage_dec_tables(S.T, DEC_NT);  // the kernel's only workgroup barrier
   const uint32_t off0 = off[0];
-  unsigned long long ts = HD_DIAG_STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
-  (void)ts;
-  for (uint32_t t0 = blockIdx.x * DEC_NS; t0 < n; t0 += gridDim.x * DEC_NS) {
-    COUNT(11, 1);
-    const uint32_t nstr = min(n - t0, (uint32_t)DEC_NS);
-    // ---- tile strings -> offsets, engine slots, items per string
-    uint32_t m2[2];
+  const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
+  uint32_t dctr[3] = {0, 0, 0};
+  (void)dctr;
+  for (uint32_t task = blockIdx.x * DEC_WAVES + wv; task < ntask; task += gridDim.x * DEC_WAVES) {
+    const uint32_t t0 = task * TASK_STR;
+    const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
+    // lane l: task string l
+    const bool sl = lane < nstr;
+    const uint32_t a_l = sl ? off[t0 + lane] : 0u;
+    const uint32_t b_l = sl ? off[t0 + lane + 1] : 0u;
+    if (AUTO && sl) {
+      dst_off[t0 + lane] = (uint32_t)auto_slot(a_l - off0, t0 + lane);
+      if (t0 + lane == n - 1) dst_off[n] = (uint32_t)auto_slot(b_l - off0, n);
+    }
+    const uint32_t m_l = sl ? (b_l - a_l > PIECE_BYTES ? (b_l - a_l + PIECE_BYTES - 1u) / PIECE_BYTES : 1u) : 0u;
+    const uint32_t P_l = wave_incl_scan(m_l);       // items through string l
+    const uint32_t X_l = P_l - m_l;                 // first item of string l
+    const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
+    uint32_t carry_exit = 0, carry_cnt = 0, IB_prev = 0;
+    for (uint32_t r0 = 0; r0 < M; r0 += WAVE) {
+      const uint32_t nv = min(M - r0, (uint32_t)WAVE);  // items this round
+      const uint32_t q = r0 + lane;
+      const bool valid = lane < nv;
+      // ---- this lane's item: string = first i with P_i > q
+      ItemPos it;
+      {
+        uint32_t lo = 0, hi = nstr - 1u;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t i = 2u * tid + h;
-      m2[h] = 0;
-      if (i < nstr) {
-        const uint32_t a = off[t0 + i], b = off[t0 + i + 1];
-        S.sa[i] = a;
-        if (AUTO) dst_off[t0 + i] = (uint32_t)auto_slot(a - off0, t0 + i);
-        m2[h] = b - a > PIECE_BYTES ? (b - a + PIECE_BYTES - 1u) / PIECE_BYTES : 1u;
-        if (i == nstr - 1) {
-          S.sa[nstr] = b;
-          if (AUTO && t0 + nstr == n) dst_off[n] = (uint32_t)auto_slot(b - off0, n);
+        for (int st = 0; st < 6; ++st) {
+          const uint32_t mid = (lo + hi) >> 1;
+          const uint32_t pm = __shfl(P_l, mid, 64);
+          if (pm > q) hi = mid; else lo = mid + 1u;
         }
+        it.i = min(lo, nstr - 1u);
+        it.k = q - __shfl(X_l, it.i, 64);
+        it.a = __shfl(a_l, it.i, 64);
+        it.b = __shfl(b_l, it.i, 64);
+        it.s = it.a + PIECE_BYTES * it.k;
+        it.last = it.s + PIECE_BYTES >= it.b;
       }
-    }
-    {
-      uint32_t tot;
-      const uint32_t ex = block_excl_scan<DEC_NT>(m2[0] + m2[1], S.red, &tot);
-      S.sbase[2u * tid] = ex;
-      S.sbase[2u * tid + 1] = ex + m2[0];
-      if (tid == 0) {
-        S.sbase[DEC_NS] = tot;
-        S.carry[0] = 0;
-        S.carry[1] = 0;
-      }
-      __syncthreads();
-    }
-    const uint32_t nitems = S.sbase[DEC_NS];
-    uint32_t IB_prev = 0;
-    STAMP(0, ts);
-    for (uint32_t r0 = 0; r0 < nitems; r0 += DEC_NT) {
-      COUNT(10, 1);
-      const uint32_t nr = min(nitems - r0, (uint32_t)DEC_NT);  // items this round
-      // ---- items of the round in order (thread t <-> item r0 + t): sort key,
-      // head flags, the round's first input byte
-      uint32_t key = 0;
-      if (tid < nr) {
-        const uint32_t q = r0 + tid;
-        const uint32_t i = find_string(S.sbase, nstr, q);
-        const uint32_t k = q - S.sbase[i];
-        const uint32_t a = S.sa[i], b = S.sa[i + 1];
-        const uint32_t s = a + PIECE_BYTES * k;
-        key = min(b - s, PIECE_BYTES) + (k ? SUB_OV : 0u);
-        S.head[tid] = k == 0;
-        if (tid == 0) {
-          S.rinfo[0] = k ? s - SUB_OV : s;
-          S.rinfo[1] = i;
-        }
-      }
-      if (tid < 128) S.hist[tid] = 0;
-      if (tid == 0) S.qmax = 0;
-      __syncthreads();
-      const uint32_t A = S.rinfo[0], i0 = S.rinfo[1];
+      // ---- stage the round's input: [first item (- warm-up), last item's reach)
+      const uint32_t A = __builtin_amdgcn_readlane(it.k ? it.s - SUB_OV : it.s, 0);
+      const uint32_t Z = __builtin_amdgcn_readlane(min(it.b, it.s + PIECE_BYTES), nv - 1u) + 12u;
       const uint32_t IB = A & ~15u;
       const uint32_t IBX = IB - 16u;  // bit positions: 8 * (byte - IBX) >= 128
-      {  // ---- stage the round's input [IB, IB + IBUF_BYTES) within the pool contract
-        const uint32_t lim = ((S.sa[nstr] + 15u) & ~15u) + 16u;
-        const uint32_t nchunk = (min(IB + IBUF_BYTES, lim) - IB) >> 4;
+      {
+        const uint32_t nchunk = (((Z + 15u) & ~15u) - IB) >> 4;
         const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
-        for (uint32_t c = tid; c < nchunk; c += DEC_NT) {
+        for (uint32_t c = lane; c < nchunk; c += WAVE) {
           const uint4 v = g[c];
-          reinterpret_cast<uint4 *>(S.ibe)[c + 1] =
-              make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
-                         __builtin_bswap32(v.w));
+          reinterpret_cast<lds_u32 *>(ibw)[4u * c + 4u] = __builtin_bswap32(v.x);
+          reinterpret_cast<lds_u32 *>(ibw)[4u * c + 5u] = __builtin_bswap32(v.y);
+          reinterpret_cast<lds_u32 *>(ibw)[4u * c + 6u] = __builtin_bswap32(v.z);
+          reinterpret_cast<lds_u32 *>(ibw)[4u * c + 7u] = __builtin_bswap32(v.w);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       // the carried exit is a bit position of the previous round's staging
-      uint32_t carry_exit = S.carry[0];
       if (carry_exit < NOSPEC) carry_exit -= 8u * (IB - IB_prev);
       IB_prev = IB;
-      const uint32_t carry_cnt = S.carry[1];
-      // ---- the round's output image [P, U) (uniform)
-      uint64_t OB = 0, P = 0;
-      bool staged = false;
-      if (AUTO) {
-        P = auto_slot(S.sa[i0] - off0, t0 + i0) + (S.head[0] ? 0u : carry_cnt);
-        const uint32_t il = find_string(S.sbase, nstr, r0 + nr - 1);
-        const uint64_t U = auto_slot(S.sa[il + 1] - off0, t0 + il + 1);
-        OB = P & ~(uint64_t)15u;
-        staged = HD_DEC_OUTSTAGE && U - OB <= DEC_OBUF && U <= dst_cap;
-      }
-      // ---- length-sorted assignment: thread t decodes item r0 + perm[t]
-      uint32_t rank = 0;
-      if (tid < nr) rank = atomicAdd(&S.hist[key], 1u);
-      __syncthreads();
-      {
-        uint32_t tot;
-        const uint32_t h = tid < 128 ? S.hist[tid] : 0u;
-        const uint32_t ex = block_excl_scan<DEC_NT>(h, S.red, &tot);
-        if (tid < 128) S.hist[tid] = ex;
-        __syncthreads();
-        if (tid < nr) S.perm[S.hist[key] + rank] = (uint16_t)tid;
-        __syncthreads();
-      }
-      STAMP(1, ts);
-      const bool valid = tid < nr;
-      const uint32_t u = valid ? S.perm[tid] : 0u;
-      const uint32_t q = r0 + u;
-      const uint32_t i = find_string(S.sbase, nstr, q), j = t0 + i;
-      const uint32_t k = q - S.sbase[i];
-      const uint32_t a = S.sa[i], b = S.sa[i + 1];
-      const uint32_t s = a + PIECE_BYTES * k;
-      const bool last = s + PIECE_BYTES >= b;
-      const uint32_t bseg = 8u * (s - IBX);
-      const uint32_t bend = 8u * (min(b, s + PIECE_BYTES + 32u) - IBX);
-      const uint32_t bstop = last ? bend : 8u * (s + PIECE_BYTES - IBX);
+      const uint32_t j = t0 + it.i;
+      const uint32_t bseg = 8u * (it.s - IBX);
+      const uint32_t bend = 8u * (min(it.b, it.s + PIECE_BYTES + 32u) - IBX);
+      const uint32_t bstop = it.last ? bend : 8u * (it.s + PIECE_BYTES - IBX);
       bool slot_ovf = false;  // AUTO: the string's slot is beyond dst_cap
       uint64_t o = 0;
       uint32_t cap = 0;
-      if (AUTO) {
-        o = auto_slot(a - off0, j);
-        slot_ovf = auto_slot(b - off0, j + 1) > dst_cap;
-      } else {
-        o = dst_off[j];
-        cap = dst_off[j + 1] - (uint32_t)o;
-      }
-      uint32_t qend = 0;  // end of this lane's output (relative to OB)
-      uint32_t dctr[3] = {0, 0, 0};
-      // ---- pass 1: k = 0 exact (written); k > 0 speculative count
       if (valid) {
-        SubOut r;
+        if (AUTO) {
+          o = auto_slot(it.a - off0, j);
+          slot_ovf = auto_slot(it.b - off0, j + 1) > dst_cap;
+        } else {
+          o = dst_off[j];
+          cap = dst_off[j + 1] - (uint32_t)o;
+        }
+      }
+      // ---- pass 1: k = 0 exact (written); k > 0 speculative count
+      SubOut r;
+      r.entry = r.exit = XFAIL;
+      r.cnt = 0;
+      r.t = r.win = 0;
+      r.at_end = false;
+      if (valid) {
         bool ovf = false;
-        if (k == 0) {
+        if (it.k == 0) {
           if (slot_ovf) {
-            r.entry = r.exit = XFAIL;
-            r.cnt = 0;
             ovf = true;
           } else if (!AUTO) {
             CheckedSink sk;
             sk.init(dst + o, cap);
             r = decode_item<false>(S.T, ibe, bseg, bseg, bstop, bend, sk, dctr);
             ovf = sk.ovf;
-          } else if (staged) {
-            LdsSink<false> sk;
-            sk.p = (lds_u8 *)obuf + (uint32_t)(o - OB);
-            r = decode_item<false>(S.T, ibe, bseg, bseg, bstop, bend, sk, dctr);
-            qend = (uint32_t)(o - OB) + r.cnt;
           } else {
             DwordSink sk;
             sk.init(dst + o);
             r = decode_item<false>(S.T, ibe, bseg, bseg, bstop, bend, sk, dctr);
-            sk.finish(last);
+            sk.finish(it.last);
           }
-          if (last) {
+          if (it.last) {
             uint32_t fs = 0, fl = 0;
             status[j] = finish_string(S.T, r, r.cnt, ovf, &fs, &fl);
             if (fstate_out) fstate_out[j] = (uint16_t)fs;
@@ -932,166 +865,83 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
           NullSink nk;
           r = decode_item<true>(S.T, ibe, bseg - 8u * SUB_OV, bseg, bstop, bend, nk, dctr);
         }
-        S.es[u] = r.entry;
-        S.xs[u] = r.exit;
-        S.cs[u] = r.cnt;
       }
-#if HD_DIAG_STAMPS
-      {
-        uint32_t m0 = dctr[0], m1 = dctr[1], m2x = dctr[2];
-        for (int d = 32; d; d >>= 1) {
-          m0 = max(m0, (uint32_t)__shfl_xor(m0, d, 64));
-          m1 = max(m1, (uint32_t)__shfl_xor(m1, d, 64));
-          m2x = max(m2x, (uint32_t)__shfl_xor(m2x, d, 64));
-        }
-        if ((tid & 63) == 0) {
-          atomicAdd(&g_stamps[blockIdx.x & 4095][12], (unsigned long long)m0);
-          atomicAdd(&g_stamps[blockIdx.x & 4095][13], (unsigned long long)m1);
-          atomicAdd(&g_stamps[blockIdx.x & 4095][14], (unsigned long long)m2x);
-        }
-      }
-#endif
-      __syncthreads();
-      STAMP(2, ts);
-      // ---- verify / redo: entry of item (i, k > 0) must equal the exit of
-      // item (i, k - 1), the previous item (or the carry).  A mismatched
-      // item is re-decoded once its predecessor is settled (not itself
-      // mismatched in this iteration); the first item of the round and k = 0
-      // items are always settled, so each iteration settles at least the
-      // first mismatch.
-      for (uint32_t it = 0; it <= DEC_NT; ++it) {
-        bool mism = false;
-        uint32_t pred = 0;
-        if (valid && k > 0) {
-          pred = u ? S.xs[u - 1] : carry_exit;
-          const uint32_t e0 = S.es[u];
-          mism = e0 != pred || e0 == XUNKNOWN;
-        }
-        if (valid) S.unsettled[u] = mism ? 1u : 0u;
-        const bool any = __syncthreads_or(mism);
-#if HD_DIAG_STAMPS
-        { const unsigned long long nm = __syncthreads_count(mism); COUNT(9, nm); COUNT(8, 1); }
-#endif
-        if (!any) break;
-        if (mism && (u == 0 || !S.unsettled[u - 1])) {
-          SubOut rr;
-          rr.cnt = 0;
+      // ---- verify / redo (wave): the entry of item (i, k > 0) must equal
+      // the exit of the previous lane's item (i, k - 1), or the carry.  A
+      // mismatched item is re-decoded once its predecessor is settled (not
+      // itself mismatched in this iteration); lane 0 is always settled.
+      for (uint32_t iter = 0; iter <= WAVE; ++iter) {
+        const uint32_t up = __shfl_up(r.exit, 1, 64);
+        const uint32_t pred = lane ? up : carry_exit;
+        const bool mism = valid && it.k > 0 && (r.entry != pred || r.entry == XUNKNOWN);
+        const uint64_t bal = __ballot(mism);
+        if (bal == 0) break;
+        const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
+        if (mism && !pred_mism) {
           if (pred == XFAIL || pred == XUNKNOWN) {
-            rr.entry = rr.exit = XFAIL;
+            r.entry = r.exit = XFAIL;
+            r.cnt = 0;
           } else {
             NullSink nk;
-            rr = decode_item<false>(S.T, ibe, pred, bseg, bstop, bend, nk, dctr);
+            r = decode_item<false>(S.T, ibe, pred, bseg, bstop, bend, nk, dctr);
           }
-          S.es[u] = rr.entry;
-          S.xs[u] = rr.exit;
-          S.cs[u] = rr.cnt;
         }
-        __syncthreads();
       }
-      STAMP(3, ts);
       // ---- symbols of each string through each item: segmented inclusive
-      // scan in item order, segments headed by k = 0 items; the first
-      // segment continues the carry.
-      {
-        const bool live = tid < nr;
-        const uint32_t v = live ? S.cs[tid] : 0u;
-        const int32_t h = (!live || S.head[tid]) ? (int32_t)tid : -1;
-        uint32_t ps = v;
-        int32_t hm = h;
-        const uint32_t lane = tid & 63u, wv = tid >> 6;
+      // scan over lanes, segments headed by k = 0 items; the first segment
+      // continues the carry
+      const uint32_t v = valid ? r.cnt : 0u;
+      uint32_t ps = v;
+      int32_t hm = (!valid || it.k == 0) ? (int32_t)lane : -1;
 #pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-          const uint32_t o2 = __shfl_up(ps, d, 64);
-          const int32_t oh = __shfl_up(hm, d, 64);
-          if (lane >= d) {
-            ps += o2;
-            hm = max(hm, oh);
-          }
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o2 = __shfl_up(ps, d, 64);
+        const int32_t oh = __shfl_up(hm, d, 64);
+        if (lane >= d) {
+          ps += o2;
+          hm = max(hm, oh);
         }
-        if (lane == 63) {
-          S.red[wv] = ps;
-          S.red[DEC_NT / 64 + wv] = (uint32_t)hm;
-        }
-        __syncthreads();
-        for (uint32_t w = 0; w < wv; ++w) {
-          ps += S.red[w];
-          hm = max(hm, (int32_t)S.red[DEC_NT / 64 + w]);
-        }
-        S.seg[tid] = ps;  // inclusive prefix
-        __syncthreads();
-        const uint32_t base = hm >= 0 ? S.seg[hm] - (hm < (int32_t)nr ? S.cs[hm] : 0u) : 0u - carry_cnt;
-        __syncthreads();
-        S.seg[tid] = ps - base;
-        __syncthreads();
       }
-      STAMP(4, ts);
+      const uint32_t excl_h = __shfl(ps - v, hm >= 0 ? (uint32_t)hm : 0u, 64);
+      const uint32_t seg = hm >= 0 ? ps - excl_h : ps + carry_cnt;
       // ---- pass 2: k > 0 exact, at the string's running symbol count
-      if (valid && k > 0) {
-        const uint32_t soff = S.seg[u] - S.cs[u];
-        const uint32_t e0 = S.es[u];
-        SubOut r;
-        r.entry = r.exit = XFAIL;
-        r.cnt = 0;
-        r.t = r.win = 0;
-        r.at_end = false;
+      if (valid && it.k > 0) {
+        const uint32_t soff = seg - r.cnt;
+        const uint32_t e0 = r.entry;
+        SubOut r2;
+        r2.entry = r2.exit = XFAIL;
+        r2.cnt = 0;
+        r2.t = r2.win = 0;
+        r2.at_end = false;
         bool ovf = AUTO && slot_ovf;
         if (e0 != XFAIL && !ovf) {
           if (!AUTO) {
             CheckedSink sk;
             sk.init(dst + o + min(soff, cap), cap > soff ? cap - soff : 0u);
-            r = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
-            ovf = soff + r.cnt > cap;  // this piece or an earlier one overflowed
-          } else if (staged) {
-            LdsSink<true> sk;
-            sk.p = (lds_u8 *)obuf + (uint32_t)(o + soff - OB);
-            sk.junk = junk;
-            r = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
-            qend = (uint32_t)(o + soff - OB) + r.cnt;
+            r2 = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
+            ovf = soff + r2.cnt > cap;  // this piece or an earlier one overflowed
           } else {
             GlobalSink sk;
             sk.p = dst + o + soff;
-            r = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
+            r2 = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
           }
         } else if (!AUTO) {
           ovf = soff > cap;
         }
-        if (last) {
+        if (it.last) {
           uint32_t fs = 0, fl = 0;
-          status[j] = finish_string(S.T, r, soff + r.cnt, ovf, &fs, &fl);
+          status[j] = finish_string(S.T, r2, soff + r2.cnt, ovf, &fs, &fl);
           if (fstate_out) fstate_out[j] = (uint16_t)fs;
           if (flags_out) flags_out[j] = (uint8_t)fl;
         }
       }
-      if (staged && qend) atomicMax(&S.qmax, qend);
-      __syncthreads();
-      STAMP(5, ts);
       // ---- carry the string running into the next round
-      if (tid == 0) {
-        S.carry[0] = S.xs[nr - 1];
-        S.carry[1] = S.seg[nr - 1];
-      }
-      // ---- store the round's image [P, OB + qmax): whole 16-byte words,
-      // partial words at either end bytewise (their other bytes belong to
-      // the neighbouring rounds)
-      if (staged) {
-        const uint64_t hi = OB + S.qmax;
-        const lds_u8 *ob = (const lds_u8 *)obuf;
-        if (hi > P) {
-          const uint64_t wlo = (P + 15u) & ~(uint64_t)15u, whi = hi & ~(uint64_t)15u;
-          if (wlo <= whi) {
-            const uint32_t nwords = (uint32_t)((whi - wlo) >> 4);
-            uint4 *g = reinterpret_cast<uint4 *>(dst + wlo);
-            const uint4 *l = reinterpret_cast<const uint4 *>(obuf) + ((wlo - OB) >> 4);
-            for (uint32_t c = tid; c < nwords; c += DEC_NT) g[c] = l[c];
-            if (tid < wlo - P) dst[P + tid] = ob[P - OB + tid];
-            if (tid >= 16 && tid - 16 < hi - whi) dst[whi + tid - 16] = ob[whi - OB + tid - 16];
-          } else if (tid < hi - P) {
-            dst[P + tid] = ob[P - OB + tid];
-          }
-        }
-      }
-      __syncthreads();
-      STAMP(6, ts);
+      carry_exit = __builtin_amdgcn_readlane(r.exit, nv - 1u);
+      carry_cnt = __builtin_amdgcn_readlane(seg, nv - 1u);
+      // the next round overwrites the staged input
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }
@@ -1266,7 +1116,7 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                                      void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !dst || !dst_off || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid<k_decode<false>, DEC_NT, DEC_NS>(n)), dim3(DEC_NT), 0,
+  hipLaunchKernelGGL(k_decode<false>, dim3(persistent_grid<k_decode<false>, DEC_NT, TASK_STR * DEC_WAVES>(n)), dim3(DEC_NT), 0,
                      (hipStream_t)stream, src, src_off, n, dst, (uint64_t)0,
                      (uint32_t *)dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
@@ -1280,7 +1130,7 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>, DEC_NT, DEC_NS>(n)), dim3(DEC_NT), 0, st, src, src_off,
+  hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>, DEC_NT, TASK_STR * DEC_WAVES>(n)), dim3(DEC_NT), 0, st, src, src_off,
                      n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());
 }

@@ -191,6 +191,23 @@ def build():
                 assert L2 <= 7
                 e = s1 | (L1 << 8) | (L2 << 13) | (s2 << 16) | (2 << 24) | ((L1 + L2) << 27)
         lut.append(e)
+    # second level for codes of 13..16 bits: every code longer than 12 bits
+    # starts with 10 ones; indexed by the 6 window bits after them.  Entry as
+    # above with cnt 1 (sym | L << 8 | 1 << 24 | L << 27); 0 = longer code.
+    lut2 = []
+    for v in range(64):
+        w16 = (0x3FF << 6) | v
+        e = 0
+        for L in range(LUT_BITS + 1, 17):
+            sym = leaf.get((w16 >> (16 - L), L))
+            if sym is not None:
+                assert sym != EOS
+                e = sym | (L << 8) | (1 << 24) | (L << 27)
+                break
+        lut2.append(e)
+    for code, L in enc:
+        if L > LUT_BITS:
+            assert code >> 22 == 0x3FF, "long code without 10 leading ones"
     # long codes: (L, left-justified exclusive limit as a 32-bit-window
     # compare, first code, canonical index base) for every length > LUT_BITS
     longc = []
@@ -200,7 +217,7 @@ def build():
             longc.append((L, lim, first[L], base[L]))
     return dict(enc=enc, fsm=fsm, order=order, count=count, first=first,
                 base=base, depth_lo=depth_lo, depth_base=depth_base,
-                id_list=id_list, lut=lut, longc=longc)
+                id_list=id_list, lut=lut, lut2=lut2, longc=longc)
 
 
 def packed_ref_layout(t):
@@ -265,6 +282,11 @@ def write_inc(t, path):
     w("};")
     w("/* codes longer than the lookup: X(len, limit32 (exclusive, left-justified),"
       " first code, canonical base); limit of the last is 2^32 */")
+    w("/* second-level lookup for 13..16-bit codes: window bits 10..15 (after ten ones) */")
+    w("HD_TBL const unsigned int hd_huff_lut2[64] = {")
+    for i in range(0, 64, 8):
+        w("  " + ", ".join("0x%08Xu" % e for e in t["lut2"][i:i + 8]) + ",")
+    w("};")
     w("#define HD_HUFF_LONG_CODES(X) \\")
     for L, lim, fc, b in t["longc"]:
         w("  X(%d, 0x%XULL, 0x%Xu, %du) \\" % (L, lim, fc, b))

@@ -7,7 +7,4 @@ SRC=$HERE/../../nghttp2_amd/csrc/hd_huff.hip
 rm -f $HERE/lib_*.so
 build() { name=$1; shift; (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 "$@" -o $HERE/lib_$name.so $SRC); echo built $name; }
 build base
-build nooutstage -DHD_DEC_OUTSTAGE=0
 build window -DHD_BITBUF=0
-build win_noout -DHD_BITBUF=0 -DHD_DEC_OUTSTAGE=0
-build stamps -DHD_DIAG_STAMPS=1

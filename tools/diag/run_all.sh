@@ -8,7 +8,6 @@ timeout -k 10 400 python -m pytest tests -m gpu -q > gpurun_out/diag/pytest.log 
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/diag/pytest.log
 [ $rc -le 1 ] || exit $rc
 for c in 2 3; do
-  timeout -k 10 200 python tools/diag/stamps.py $c > gpurun_out/diag/st$c.json 2>&1 || exit $?
   timeout -k 10 200 python tools/diag/time_variants.py $c > gpurun_out/diag/tv$c.json 2>&1 || exit $?
 done
 [ -n "${NO_PMC:-}" ] || bash tools/diag/pmc_dec.sh 2

@@ -8,6 +8,7 @@ sys.path.insert(0, os.path.join(HERE, "..", ".."))
 from nghttp2_amd import workloads as W
 import nghttp2_amd
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+WPG = 8  # waves per decode workgroup (DEC_NT / 64)
 dev = torch.device("cuda:0")
 pool, off = W.gen_pseudo_headers(1 << 20) if cfg == 2 else W.gen_mixed_values(1 << 20)
 codec = nghttp2_amd.HuffmanBatchCodec(dev)
@@ -38,7 +39,7 @@ print(json.dumps({"config": cfg, "wgs": int(used.sum()),
                   "verify_iters_per_round": float(buf[:, 8].sum() / max(1, buf[:, 10].sum())),
                   "mismatches_per_round": float(buf[:, 9].sum() / max(1, buf[:, 10].sum())),
                   "rounds": int(buf[:, 10].sum()), "tiles": int(buf[:, 11].sum()),
-                  "wave_trips_per_round": {"fast": float(buf[:, 12].sum() / max(1, buf[:, 10].sum()) / 4),
-                                           "checked": float(buf[:, 13].sum() / max(1, buf[:, 10].sum()) / 4),
-                                           "warm": float(buf[:, 14].sum() / max(1, buf[:, 10].sum()) / 4)},
-                  "wave_pass1_cycles_per_round": float(buf[:, 15].sum() / max(1, buf[:, 10].sum()) / 4)}, indent=1))
+                  "wave_trips_per_round": {"fast": float(buf[:, 12].sum() / max(1, buf[:, 10].sum()) / WPG),
+                                           "checked": float(buf[:, 13].sum() / max(1, buf[:, 10].sum()) / WPG),
+                                           "warm": float(buf[:, 14].sum() / max(1, buf[:, 10].sum()) / WPG)},
+                  "wave_pass1_cycles_per_round": float(buf[:, 15].sum() / max(1, buf[:, 10].sum()) / WPG)}, indent=1))
