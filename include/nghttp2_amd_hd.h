@@ -84,6 +84,12 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, u
  * nghttp2_amd_hd_huff_decode_slots need for `n` strings. */
 NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
 
+/* Workspace that lets nghttp2_amd_hd_huff_encode_batch keep per-piece bit
+ * counts from its count pass for its pack pass (faster; same output) for
+ * `raw_bytes` raw bytes in `n` strings.  Any size >=
+ * nghttp2_amd_hd_huff_workspace_size(n) is valid. */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw_bytes, uint32_t n);
+
 /* ------------------------------------------------------------------ */
 /* Batched device-resident API                                          */
 /* ------------------------------------------------------------------ */
@@ -97,7 +103,8 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
  *   dst               : encoded pool (device), >= dst_cap bytes
  *   dst_off[n+1]      : OUT: encoded string i = dst[dst_off[i]..dst_off[i+1]);
  *                       dst_off[i+1]-dst_off[i] == nghttp2_hd_huff_encode_count
- *   workspace         : device scratch, nghttp2_amd_hd_huff_workspace_size(n)
+ *   workspace         : device scratch, >= nghttp2_amd_hd_huff_workspace_size(n);
+ *                       nghttp2_amd_hd_huff_encode_workspace_size(raw, n) is faster
  *
  * Output bytes equal lib/nghttp2_hd_huffman.c's, including the EOS-prefix
  * (all ones) padding of the last byte.  dst_cap must be >=

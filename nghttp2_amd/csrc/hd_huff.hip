@@ -45,7 +45,6 @@ namespace host {
 #define SCAN_WG 1024
 #define DEC_WG_PER_CU 8 // persistent decode grid: 256 CUs x 8 workgroups
 #define NUM_CU 256
-#define ENC_OBUF 16384  // LDS output staging per encode workgroup (bytes)
 
 // Ablation switch (tools/diag builds variants; the product uses the default)
 
@@ -148,46 +147,11 @@ struct ByteOut {
 // global output to global_* (never flat_*).
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-template <class BP> struct W32Of { typedef uint32_t type; };
-template <> struct W32Of<lds_u8 *> { typedef lds_u32 type; };
-template <class BP> using W32 = typename W32Of<BP>::type;
 
 // Word writer for encode output: the stream [o, o+E) receives big-endian
 // 32-bit groups; with phase = o & 3 fixed, each group completes one aligned
 // word (funnel shift with the pending bytes).  The head word that also holds
 // the previous string's bytes, and the tail, are written byte by byte.
-template <class BP>  // BP: byte pointer (global or LDS address space)
-struct WordOut {
-  BP base;
-  uint32_t q, o, phase, pend;
-  __device__ __forceinline__ void init(BP b, uint32_t start) {
-    base = b; q = start; o = start; phase = start & 3u; pend = 0;
-  }
-  __device__ __forceinline__ void put32(uint32_t be) {
-    const uint32_t le = __builtin_bswap32(be);
-    if (phase == 0) {
-      *reinterpret_cast<W32<BP> *>(base + q) = le;
-    } else {
-      const uint32_t word = pend | (le << (8 * phase));
-      const uint32_t wa = q & ~3u;
-      if (wa < o) {
-        for (uint32_t k = phase; k < 4; ++k) base[wa + k] = (uint8_t)(word >> (8 * k));
-      } else {
-        *reinterpret_cast<W32<BP> *>(base + wa) = word;
-      }
-      pend = le >> (8 * (4 - phase));
-    }
-    q += 4;
-  }
-  // append the top `nbytes` (0..4) bytes of `be`, then drain everything
-  __device__ __forceinline__ void finish(uint32_t be, uint32_t nbytes) {
-    if (q > o) {
-      const uint32_t wa = q & ~3u;
-      for (uint32_t k = 0; k < phase; ++k) base[wa + k] = (uint8_t)(pend >> (8 * k));
-    }
-    for (uint32_t k = 0; k < nbytes; ++k) base[q + k] = (uint8_t)(be >> (24 - 8 * k));
-  }
-};
 
 // 4 bytes at an arbitrary pool position, big-endian (first byte in bits
 // 31..24); bytes at or past `end` read as zero.  Reads stay within
@@ -202,50 +166,10 @@ __device__ __forceinline__ uint32_t load_be32(const uint8_t *base, uint32_t pos,
   return x;
 }
 
-// Same from an LDS staging buffer (byte index relative to the buffer, which
-// holds at least 8 readable bytes past every index used).
-__device__ __forceinline__ uint32_t load_be32_lds(const uint32_t *buf, uint32_t pos) {
-  const uint32_t w0 = buf[pos >> 2];
-  const uint32_t w1 = buf[(pos >> 2) + 1];
-  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
-}
 
 // ---------------------------------------------------------------------------
 // encode, pass 1: per-string encoded length  (lib/nghttp2_hd_huffman.c:34-43)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
-                                                  const uint32_t *__restrict__ off,
-                                                  uint32_t n,
-                                                  uint32_t *__restrict__ out_len,
-                                                  uint32_t *__restrict__ tile_sums) {
-  __shared__ uint8_t lenT[256];
-  __shared__ uint32_t red[WG / 64];
-  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
-  __syncthreads();
-  const uint32_t s = blockIdx.x * WG + threadIdx.x;
-  uint32_t e = 0;
-  if (s < n) {
-    const uint32_t a = off[s], b = off[s + 1];
-    uint32_t bits = 0;
-    for (uint32_t c = a & ~15u; c < b; c += 16) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(src + c);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t p = c + j;
-        const uint32_t L = lenT[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-        bits += (p >= a && p < b) ? L : 0u;
-      }
-    }
-    e = (bits + 7u) >> 3;
-    if (out_len) out_len[s] = e;
-  }
-  if (tile_sums) {
-    uint32_t tot;
-    block_excl_scan<WG>(e, red, &tot);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
-  }
-}
 
 // decode slots: cap_i = floor(8 E_i / 5) + 1 (lib/nghttp2_hd_huffman.h:76-78)
 __global__ __launch_bounds__(WG) void k_slot_len(const uint32_t *__restrict__ off, uint32_t n,
@@ -307,81 +231,335 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 // ---------------------------------------------------------------------------
 // Bit-pack one string [a, b) MSB-first (lib/nghttp2_hd_huffman.c:57-84) into
 // out_base[o ..], padding the last byte with the EOS prefix (:95-101).
-template <class BP>
-__device__ __forceinline__ void encode_one(const uint2 *codeT, const uint8_t *__restrict__ src,
-                                           uint32_t a, uint32_t b, BP out_base, uint32_t o) {
-  uint64_t acc = 0;  // MSB-aligned pending bits, nb < 32 between bytes
-  uint32_t nb = 0;
-  WordOut<BP> out;
-  out.init(out_base, o);
-  for (uint32_t c = a & ~15u; c < b; c += 16) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(src + c);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// ---------------------------------------------------------------------------
+// encode (lib/nghttp2_hd_huffman.c:34-104), balanced by raw bytes.  A wave
+// owns 64 consecutive strings (lane i <-> string i) and walks their PIECES
+// of ENC_PIECE raw bytes in rounds of 64 (one per lane), so every lane
+// handles <= 32 input bytes per round whatever the string lengths.
+// ---------------------------------------------------------------------------
+#ifndef ENC_PIECE
+#define ENC_PIECE 32u
+#endif
+#define ENC_PW (ENC_PIECE / 4)       // dwords per piece
+#define ENC_PC (ENC_PIECE / 16 + 1)  // aligned chunks covering a piece
+#define ENC_WAVES 4                  // waves per encode workgroup (tile = 256 strings)
+#define ENC_REGION 4096u             // per-wave LDS output staging (bytes)
+
+struct EncPiece {
+  uint32_t i, k, s, e;  // wave string, piece, raw bytes [s, e)
+  uint32_t a;           // the string's first raw byte
+  bool last;            // the string's last piece
+};
+
+// Piece q of the wave's strings: string = first i with P_i > q.
+__device__ __forceinline__ EncPiece enc_piece(uint32_t q, uint32_t nstr, uint32_t P_l, uint32_t X_l,
+                                              uint32_t a_l, uint32_t b_l) {
+  uint32_t lo = 0, hi = nstr - 1u;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t p = c + j;
-      if (p >= a && p < b) {
-        const uint2 e = codeT[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-        acc |= (uint64_t)e.x << (32 - nb);
-        nb += e.y;
-        if (nb >= 32) {
-          out.put32((uint32_t)(acc >> 32));
-          acc <<= 32;
-          nb -= 32;
-        }
+  for (int st = 0; st < 6; ++st) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint32_t pm = __shfl(P_l, mid, 64);
+    if (pm > q) hi = mid; else lo = mid + 1u;
+  }
+  EncPiece p;
+  p.i = min(lo, nstr - 1u);
+  p.k = q - __shfl(X_l, p.i, 64);
+  const uint32_t a = __shfl(a_l, p.i, 64), b = __shfl(b_l, p.i, 64);
+  p.a = a;
+  p.s = a + ENC_PIECE * p.k;
+  p.e = min(b, p.s + ENC_PIECE);
+  p.last = p.s + ENC_PIECE >= b;
+  return p;
+}
+
+// A piece's bytes, realigned so that byte j of the piece is byte j of w[]:
+// the three aligned 16-byte chunks covering it are loaded (only those that
+// hold piece bytes -- the pool contract ends at align16(off[n]) + 16), then
+// shifted by the piece's offset in its first chunk.
+struct PieceBytes {
+  uint32_t w[ENC_PW];
+  uint32_t len;  // piece bytes (<= ENC_PIECE)
+  __device__ __forceinline__ void load(const uint8_t *src, const EncPiece &p, bool valid) {
+    const uint32_t c0 = p.s & ~15u;
+    const uint4 *g = reinterpret_cast<const uint4 *>(src + c0);
+    len = valid ? p.e - p.s : 0u;
+    uint32_t x[4 * ENC_PC];
+#pragma unroll
+    for (int c = 0; c < ENC_PC; ++c) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (valid && p.e > c0 + 16u * c) v = g[c];
+      x[4 * c] = v.x; x[4 * c + 1] = v.y; x[4 * c + 2] = v.z; x[4 * c + 3] = v.w;
+    }
+    const uint32_t d = p.s & 15u, q = d >> 2, r = 8u * (d & 3u);
+    // y[k] = x[k + q] for k = 0..ENC_PW (q in 0..3): selects, no runtime indexing
+    uint32_t y[ENC_PW + 1];
+#pragma unroll
+    for (int k = 0; k <= ENC_PW; ++k) {
+      const uint32_t a0 = x[k], a1 = x[k + 1], a2 = x[k + 2], a3 = (k + 3 < 4 * ENC_PC) ? x[k + 3] : 0u;
+      y[k] = (q & 2u) ? ((q & 1u) ? a3 : a2) : ((q & 1u) ? a1 : a0);
+    }
+#pragma unroll
+    for (int k = 0; k < ENC_PW; ++k)
+      w[k] = r ? (uint32_t)((((uint64_t)y[k + 1] << 32) | y[k]) >> r) : y[k];
+  }
+  __device__ __forceinline__ uint32_t byte(int j) const { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
+};
+
+// Code bits of a piece; jmax: the wave's longest piece (uniform loop bound).
+__device__ __forceinline__ uint32_t piece_bits(const PieceBytes &pb, const uint8_t *lenT, uint32_t jmax) {
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < ENC_PW; ++k) {
+    if ((uint32_t)(4 * k) < jmax) {  // uniform
+      const uint32_t wd = pb.w[k];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t L = lenT[(wd >> (8 * b)) & 0xFFu];
+        bits += ((uint32_t)(4 * k + b) < pb.len) ? L : 0u;
       }
     }
   }
-  const uint32_t pad = (8u - (nb & 7u)) & 7u;
-  acc |= (~0ull >> nb) & ~(~0ull >> (nb + pad));
-  nb += pad;
-  out.finish((uint32_t)(acc >> 32), nb >> 3);
+  return bits;
 }
 
+// Uniform maximum over the wave.
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Per-string encoded lengths (and per-tile sums): pass 1 of the batch.
+// Piece slot in the optional per-piece bit-count array: the pieces before
+// string s number <= (off[s] - off[0]) / ENC_PIECE + s, so
+// slot(s, k) = (off[s] - off[0]) / ENC_PIECE + s + k is unique and
+// increasing; the array holds enc_piece_slots(raw_bytes, n) entries.
+__device__ __host__ __forceinline__ uint64_t enc_piece_slot(uint32_t rel, uint32_t s, uint32_t k) {
+  return (uint64_t)(rel / ENC_PIECE) + s + k;
+}
+
+__global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
+                                                  const uint32_t *__restrict__ off,
+                                                  uint32_t n,
+                                                  uint32_t *__restrict__ out_len,
+                                                  uint32_t *__restrict__ tile_sums,
+                                                  uint16_t *__restrict__ piece_bits_out) {
+  __shared__ uint8_t lenT[256];
+  __shared__ uint32_t sbits[ENC_WAVES][64];
+  __shared__ uint32_t red[WG / 64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+  sbits[wv][lane] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;  // the wave's strings
+  uint32_t e = 0;
+  if (t0 < n) {
+    const uint32_t nstr = min(n - t0, 64u);
+    const bool sl = lane < nstr;
+    const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+    const uint32_t m_l = sl ? max(1u, (b_l - a_l + ENC_PIECE - 1u) / ENC_PIECE) : 0u;
+    const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
+    const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
+    const uint32_t off0 = off[0];
+    for (uint32_t r0 = 0; r0 < M; r0 += 64u) {
+      const bool valid = r0 + lane < M;
+      const EncPiece p = enc_piece(r0 + lane, nstr, P_l, X_l, a_l, b_l);
+      PieceBytes pb;
+      pb.load(src, p, valid);
+      const uint32_t bits = piece_bits(pb, lenT, wave_max(pb.len));
+      if (valid) {
+        atomicAdd(&sbits[wv][p.i], bits);
+        if (piece_bits_out)
+          piece_bits_out[enc_piece_slot(p.a - off0, t0 + p.i, p.k)] = (uint16_t)bits;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (sl) {
+      e = (sbits[wv][lane] + 7u) >> 3;
+      if (out_len) out_len[t0 + lane] = e;
+    }
+  }
+  if (tile_sums) {
+    uint32_t tot;
+    block_excl_scan<WG>(e, red, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+  }
+}
+
+// Pack: dst_off holds the encoded lengths on entry, the string offsets on
+// exit.  Each round's output -- contiguous, since pieces and strings are --
+// is assembled in the wave's LDS region with ds_or (pieces meet at
+// arbitrary bits) and stored with dwords; bytes shared with a neighbouring
+// wave or tile go bytewise, and a byte shared with the wave's previous
+// round is carried.
 __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_prefix) {
+                                               const uint32_t *__restrict__ tile_prefix,
+                                               const uint16_t *__restrict__ piece_bits_in) {
   __shared__ uint2 codeT[256];
+  __shared__ uint8_t lenT[256];
+  __shared__ uint32_t region[ENC_WAVES][ENC_REGION / 4];
   __shared__ uint32_t red[WG / 64];
-  __shared__ uint32_t obuf[ENC_OBUF / 4];
-  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x],
-                                  dev::hd_huff_enc_len[threadIdx.x]);
-  const uint32_t s = blockIdx.x * WG + threadIdx.x;
-  const uint32_t E = (s < n) ? dst_off[s] : 0u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
+  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
+  const uint32_t E_me = s_me < n ? dst_off[s_me] : 0u;
   uint32_t tot;
-  const uint32_t O0 = tile_prefix[blockIdx.x];
-  const uint32_t o = O0 + block_excl_scan<WG>(E, red, &tot);
-  const uint32_t Oend = O0 + tot;
-  const uint32_t base = O0 & ~3u;
-  // The tile's output [O0, Oend) is contiguous: stage it in LDS and store it
-  // with coalesced dwords (byte stores only for the two edge words shared
-  // with the neighbouring tiles).  Uniform across the workgroup.
-  const bool staged = (Oend - base) <= ENC_OBUF && (uint64_t)Oend <= dst_cap;
-  if (s < n) {
-    dst_off[s] = o;
-    if (staged) {
-      encode_one(codeT, src, off[s], off[s + 1], (lds_u8 *)obuf, o - base);
-    } else if ((uint64_t)o + E <= dst_cap) {  // never write past the pool
-      encode_one(codeT, src, off[s], off[s + 1], dst, o);
+  const uint32_t o_me = tile_prefix[blockIdx.x] + block_excl_scan<WG>(E_me, red, &tot);  // (barrier)
+  if (s_me < n) dst_off[s_me] = o_me;
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
+  if (t0 >= n) return;
+  lds_u32 *reg = (lds_u32 *)region[wv];
+  const uint32_t nstr = min(n - t0, 64u);
+  const bool sl = lane < nstr;
+  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+  const uint32_t m_l = sl ? max(1u, (b_l - a_l + ENC_PIECE - 1u) / ENC_PIECE) : 0u;
+  const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
+  const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
+  uint32_t carry_bits = 0;              // bits of the string running into this round
+  uint64_t carry_byte_at = ~0ull;       // global index of a byte shared with the previous round
+  uint32_t carry_byte = 0;
+  for (uint32_t r0 = 0; r0 < M;) {
+    const uint32_t q = r0 + lane;
+    const bool live = q < M;
+    const EncPiece p = enc_piece(q, nstr, P_l, X_l, a_l, b_l);
+    PieceBytes pb;
+    pb.load(src, p, live);
+    const uint32_t jmax = wave_max(pb.len);
+    uint32_t pbits;
+    if (piece_bits_in) {  // from the count pass
+      pbits = live ? piece_bits_in[enc_piece_slot(p.a - off[0], t0 + p.i, p.k)] : 0u;
+    } else {
+      pbits = live ? piece_bits(pb, lenT, jmax) : 0u;
     }
-  }
-  if (staged) {
-    __syncthreads();
-    const uint32_t nwords = (Oend - base + 3u) >> 2;
-    for (uint32_t i = threadIdx.x; i < nwords; i += WG) {
-      const uint32_t ga = base + 4u * i;
-      const uint32_t w = obuf[i];
-      if (ga >= O0 && ga + 4u <= Oend) {
-        *reinterpret_cast<uint32_t *>(dst + ga) = w;
-      } else {
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t q = ga + k;
-          if (q >= O0 && q < Oend) dst[q] = (uint8_t)(w >> (8 * k));
+    // bit offset of the piece in its string: segmented exclusive scan over
+    // lanes (segments start at k = 0), the first segment continues the carry
+    uint32_t ps = pbits;
+    int32_t hm = (!live || p.k == 0) ? (int32_t)lane : -1;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t o2 = __shfl_up(ps, d, 64);
+      const int32_t oh = __shfl_up(hm, d, 64);
+      if (lane >= d) {
+        ps += o2;
+        hm = max(hm, oh);
+      }
+    }
+    const uint32_t excl_h = __shfl(ps - pbits, hm >= 0 ? (uint32_t)hm : 0u, 64);
+    const uint32_t poff = (hm >= 0 ? ps - excl_h : ps + carry_bits) - pbits;
+    const uint32_t tbits = poff + pbits;                      // string bits through this piece
+    const uint32_t pad = p.last ? ((8u - (tbits & 7u)) & 7u) : 0u;
+    const uint64_t ostr = (uint64_t)__shfl(o_me, p.i, 64);   // o of wave string p.i (lane p.i)
+    const uint64_t gbit = 8ull * ostr + poff;                 // first output bit of the piece
+    const uint64_t gend = gbit + pbits + pad;
+    // round size: as many pieces as fit the region
+    const uint64_t B0 = __builtin_amdgcn_readlane((uint32_t)(gbit >> 3), 0) |
+                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbit >> 35), 0) << 32);
+    const uint64_t D0 = B0 & ~3ull;
+    const bool fits = live && ((gend + 7u) >> 3) - D0 + 8u <= ENC_REGION;
+    const uint64_t fitmask = __ballot(fits);
+    const uint32_t nv = ~fitmask ? (uint32_t)__builtin_ctzll(~fitmask) : 64u;  // leading lanes that fit (>= 1)
+    const bool act = lane < nv;
+    const uint32_t lastl = nv - 1u;
+    const uint64_t B1 = (uint64_t)__builtin_amdgcn_readlane((uint32_t)((gend + 7u) >> 3), lastl) |
+                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(((gend + 7u) >> 3) >> 32), lastl) << 32);
+    // zero the region's words, then OR every piece's bits in
+    const uint32_t ndw = (uint32_t)((B1 - D0 + 3u) >> 2);
+    for (uint32_t x = lane; x <= ndw; x += 64u) reg[x] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // Big-endian region words.  A piece's first and last words may hold
+    // neighbouring pieces' bits: ORed in at the end (LDS atomics).  Its
+    // interior words are its own: each is stored when it completes.  The
+    // EOS-prefix padding of a string's last piece is the code at index len.
+    if (act && gend > gbit) {
+      const uint32_t rb0 = (uint32_t)(gbit - 8ull * D0);      // region-relative bits
+      const uint32_t rbe = (uint32_t)(gend - 8ull * D0);
+      const uint32_t w0 = rb0 >> 5, wl = (rbe - 1u) >> 5;     // first and last word
+      uint32_t rb = rb0, cw = 0, first_val = 0, last_val = 0;
+      const uint32_t padcode = pad ? (~0u) << (32u - pad) : 0u;
+      // one step: append a code of len bits at rb
+#define ENC_STEP(CODE, LEN)                                                      \
+      do {                                                                     \
+        const uint32_t code_ = (CODE), len_ = (LEN);                           \
+        const uint32_t o_ = rb & 31u;                                          \
+        const uint64_t v_ = ((uint64_t)code_ << 32) >> o_;                     \
+        cw |= (uint32_t)(v_ >> 32);                                            \
+        if (o_ + len_ >= 32u) { /* word rb >> 5 complete */                    \
+          const uint32_t wd_ = rb >> 5;                                        \
+          if (wd_ != w0 && wd_ != wl) reg[wd_] = cw;                           \
+          first_val = wd_ == w0 ? cw : first_val;                              \
+          last_val = (wd_ == wl && wd_ != w0) ? cw : last_val;                 \
+          cw = (uint32_t)v_;                                                   \
+        }                                                                      \
+        rb += len_;                                                            \
+      } while (0)
+#pragma unroll
+      for (int k = 0; k < ENC_PW; ++k) {
+        if ((uint32_t)(4 * k) <= jmax) {  // uniform
+          const uint32_t wd = pb.w[k];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t j = 4 * k + b;
+            const uint2 c = codeT[(wd >> (8 * b)) & 0xFFu];
+            const bool in = j < pb.len;
+            ENC_STEP(in ? c.x : (j == pb.len ? padcode : 0u), in ? c.y : (j == pb.len ? pad : 0u));
+          }
+        }
+      }
+      if (pb.len == ENC_PIECE) ENC_STEP(padcode, pad);  // padding after a full piece
+#undef ENC_STEP
+      if (rbe & 31u) {  // the final word did not complete: cw holds its bits
+        if (wl == w0) first_val = cw; else last_val = cw;
+      }
+      atomicOr((uint32_t *)&reg[w0], first_val);
+      if (wl != w0) atomicOr((uint32_t *)&reg[wl], last_val);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // words to bytes (little-endian memory order)
+    for (uint32_t x = lane; x < ndw; x += 64u) reg[x] = __builtin_bswap32(reg[x]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // a byte shared with the previous round: merge its bits
+    if (lane == 0 && carry_byte_at == B0) {
+      lds_u8 *rb8 = (lds_u8 *)reg;
+      rb8[B0 - D0] |= (uint8_t)carry_byte;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // store [B0, B1): whole dwords, bytewise at the two ends
+    {
+      const lds_u8 *rb8 = (const lds_u8 *)reg;
+      for (uint32_t x = lane; x < ndw; x += 64u) {
+        const uint64_t ga = D0 + 4ull * x;
+        if (ga >= B0 && ga + 4u <= B1 && ga + 4u <= dst_cap) {
+          *reinterpret_cast<uint32_t *>(dst + ga) = reg[x];
+        } else {
+          for (uint32_t y = 0; y < 4; ++y) {
+            const uint64_t gq = ga + y;
+            if (gq >= B0 && gq < B1 && gq < dst_cap) dst[gq] = rb8[4u * x + y];
+          }
         }
       }
     }
+    // carry: the string running past this round, and its last partial byte
+    const uint32_t tb_last = __builtin_amdgcn_readlane(tbits, lastl);
+    const bool last_last = __builtin_amdgcn_readlane(p.last ? 1u : 0u, lastl) != 0u;
+    carry_bits = last_last ? 0u : tb_last;
+    if (!last_last && (tb_last & 7u)) {
+      carry_byte_at = B1 - 1u;
+      carry_byte = ((const lds_u8 *)reg)[B1 - 1u - D0];
+    } else {
+      carry_byte_at = ~0ull;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    r0 += nv;
   }
 }
 
@@ -1065,12 +1243,17 @@ size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n) {
   return ((size_t)ntiles_for(n) + 16u) * sizeof(uint32_t);
 }
 
+size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw_bytes, uint32_t n) {
+  const size_t slots = (size_t)enc_piece_slot(0, 0, 0) + raw_bytes / ENC_PIECE + n + 1u;
+  return nghttp2_amd_hd_huff_workspace_size(n) + ((slots * sizeof(uint16_t) + 15u) & ~(size_t)15u);
+}
+
 int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *src_off,
                                            uint32_t n, uint32_t *enc_len, void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
-                     src_off, n, enc_len, (uint32_t *)nullptr);
+                     src_off, n, enc_len, (uint32_t *)nullptr, (uint16_t *)nullptr);
   return hip_rv(hipGetLastError());
 }
 
@@ -1086,10 +1269,19 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles);
+  // Per-piece bit counts (count pass -> pack pass) when the workspace holds
+  // them for the largest raw size dst_cap admits (dst_cap >= encode_bound).
+  uint16_t *pbits = nullptr;
+  const size_t tiles_bytes = nghttp2_amd_hd_huff_workspace_size(n);
+  if (workspace_size > tiles_bytes && dst_cap > (size_t)n + 16u) {
+    const uint64_t raw_max = ((uint64_t)(dst_cap - n - 16u) * 8u) / 30u + 16u;
+    const uint64_t need = (raw_max / ENC_PIECE + n + 1u) * sizeof(uint16_t);
+    if (workspace_size - tiles_bytes >= need) pbits = (uint16_t *)((char *)workspace + tiles_bytes);
+  }
+  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, pbits);
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
   hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, (const uint16_t *)pbits);
   return hip_rv(hipGetLastError());
 }
 

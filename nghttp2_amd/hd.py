@@ -53,6 +53,8 @@ def lib():
         L.nghttp2_amd_hd_huff_encode_bound.argtypes = [ctypes.c_uint64, u32]
         L.nghttp2_amd_hd_huff_workspace_size.restype = sz
         L.nghttp2_amd_hd_huff_workspace_size.argtypes = [u32]
+        L.nghttp2_amd_hd_huff_encode_workspace_size.restype = sz
+        L.nghttp2_amd_hd_huff_encode_workspace_size.argtypes = [ctypes.c_uint64, u32]
         L.nghttp2_amd_hd_huff_encode_batch.argtypes = [vp, vp, u32, vp, sz, vp, vp, sz, vp]
         L.nghttp2_amd_hd_huff_encode_count_batch.argtypes = [vp, vp, u32, vp, vp]
         L.nghttp2_amd_hd_huff_decode_slots.argtypes = [vp, u32, vp, vp, sz, vp]
@@ -104,8 +106,11 @@ class HuffmanBatchCodec:
         self.L = lib()
         self._ws = None
 
-    def _workspace(self, n):
-        need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
+    def _workspace(self, n, raw_bytes=None):
+        if raw_bytes is None:
+            need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
+        else:
+            need = self.L.nghttp2_amd_hd_huff_encode_workspace_size(int(raw_bytes), n)
         if self._ws is None or self._ws.numel() < need:
             self._ws = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
         return self._ws
@@ -124,7 +129,7 @@ class HuffmanBatchCodec:
             dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
         if dst_off is None:
             dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
-        ws = self._workspace(n)
+        ws = self._workspace(n, raw_bytes)
         rv = self.L.nghttp2_amd_hd_huff_encode_batch(
             _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(ws),
             ws.numel(), _stream(stream))

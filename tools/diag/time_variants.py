@@ -28,12 +28,33 @@ for p in sorted(glob.glob(os.path.join(HERE, "lib_*.so"))):
     L = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
     vp = ctypes.c_void_p
     L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]
+    L.nghttp2_amd_hd_huff_encode_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp]
     libs[os.path.basename(p)[4:-3]] = L
 s = torch.cuda.current_stream()
 def run(L):
     L.nghttp2_amd_hd_huff_decode_batch_auto(ctypes.c_void_p(enc.data_ptr()), ctypes.c_void_p(eo.data_ptr()), n,
         ctypes.c_void_p(dst.data_ptr()), dcap, ctypes.c_void_p(doff.data_ptr()), ctypes.c_void_p(st.data_ptr()),
         None, None, ctypes.c_void_p(s.cuda_stream))
+ecap = codec.encode_bound(int(off[-1]), n)
+edst = torch.empty(ecap, dtype=torch.uint8, device=dev)
+eoff = torch.empty(n + 1, dtype=torch.int32, device=dev)
+wsz = codec.L.nghttp2_amd_hd_huff_encode_workspace_size(int(off[-1]), n)
+ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+def run_enc(L):
+    L.nghttp2_amd_hd_huff_encode_batch(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(so.data_ptr()), n,
+        ctypes.c_void_p(edst.data_ptr()), ecap, ctypes.c_void_p(eoff.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+        wsz, ctypes.c_void_p(s.cuda_stream))
+eres = {k: [] for k in libs}
+ref_enc = enc[:E].clone()
+for k, L in libs.items():
+    for _ in range(3): run_enc(L)
+    torch.cuda.synchronize()
+    assert torch.equal(edst[:E], ref_enc), k + ": encode differs"
+for rnd in range(10):
+    for k, L in libs.items():
+        a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+        a.record(s); run_enc(L); b.record(s); torch.cuda.synchronize()
+        eres[k].append(a.elapsed_time(b) * 1000)
 res = {k: [] for k in libs}
 for k, L in libs.items():
     for _ in range(3): run(L)
@@ -44,4 +65,5 @@ for rnd in range(10):
         a.record(s); run(L); b.record(s); torch.cuda.synchronize()
         res[k].append(a.elapsed_time(b) * 1000)
 out = {k: {"median_us": round(float(np.median(v)), 1), "min_us": round(float(np.min(v)), 1)} for k, v in res.items()}
-print(json.dumps({"config": cfg, "decode_variants": out}, indent=1))
+eout = {k: {"median_us": round(float(np.median(v)), 1), "min_us": round(float(np.min(v)), 1)} for k, v in eres.items()}
+print(json.dumps({"config": cfg, "decode_variants": out, "encode_variants": eout}, indent=1))
