@@ -632,8 +632,10 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
 #define DEC_NT (WAVE * DEC_WAVES)
 #define TASK_STR 64                                // strings per wave task
 #define PIECE_BYTES 64u                            // input bytes per item (string piece)
-#define SUB_OV 16u                                 // warm-up bytes of a k > 0 piece
-#define IBUF_W (PIECE_BYTES * WAVE + 96u)          // per-wave staged input (+ warm-up, alignment, reach)
+#ifndef SUB_OV
+#define SUB_OV 24u                                 // warm-up bytes of a k > 0 piece
+#endif
+#define IBUF_W (PIECE_BYTES * WAVE + SUB_OV + 80u)  // per-wave staged input (+ warm-up, alignment, reach)
 #define XFAIL 0xFFFFFFFFu    // exit after EOS (sticky failure)
 #define XUNKNOWN 0xFFFFFFFEu // speculative entry lost (EOS during warm-up)
 #define NOSPEC 0xFFFFFFFDu   // lane has no speculative item
@@ -701,6 +703,50 @@ struct DwordSink {
     } else {
       uint8_t *b = reinterpret_cast<uint8_t *>(p);
       for (uint32_t x = 0; x < na; ++x) b[x] = (uint8_t)(acc >> (8u * x));
+    }
+  }
+};
+// Direct global output of a piece that continues a string: its first byte
+// may share a dword with the previous piece (another lane), so that head
+// dword goes bytewise, every later complete dword whole, and the tail as
+// DwordSink::finish.
+struct UDwordSink {
+  uint32_t *p;
+  uint64_t acc;
+  uint32_t na, n, h;
+  __device__ __forceinline__ void init(uint8_t *q) {
+    h = (uint32_t)(uintptr_t)q & 3u;
+    p = reinterpret_cast<uint32_t *>(q - h);
+    acc = 0;
+    na = h;
+    n = 0;
+  }
+  __device__ __forceinline__ uint32_t count() const { return n; }
+  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
+    const uint32_t v = (e & 0xFFu) | ((e >> 8) & 0xFF00u);
+    acc |= (uint64_t)v << (8u * na);
+    na += cnt;
+    n += cnt;
+    if (na >= 4u) {
+      if (h) {  // the head dword: only bytes h..3 are this piece's
+        uint8_t *b = reinterpret_cast<uint8_t *>(p);
+        for (uint32_t x = h; x < 4u; ++x) b[x] = (uint8_t)(acc >> (8u * x));
+        h = 0;
+      } else {
+        *p = (uint32_t)acc;
+      }
+      ++p;
+      acc >>= 32;
+      na -= 4u;
+    }
+  }
+  __device__ __forceinline__ void finish(bool whole) {
+    if (na <= h) return;
+    if (whole && h == 0) {
+      *p = (uint32_t)acc;
+    } else {
+      uint8_t *b = reinterpret_cast<uint8_t *>(p);
+      for (uint32_t x = h; x < na; ++x) b[x] = (uint8_t)(acc >> (8u * x));
     }
   }
 };
@@ -1099,9 +1145,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
             r2 = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
             ovf = soff + r2.cnt > cap;  // this piece or an earlier one overflowed
           } else {
-            GlobalSink sk;
-            sk.p = dst + o + soff;
+            UDwordSink sk;
+            sk.init(dst + o + soff);
             r2 = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
+            sk.finish(it.last);
           }
         } else if (!AUTO) {
           ovf = soff > cap;

@@ -6,5 +6,5 @@ HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../../nghttp2_amd/csrc/hd_huff.hip
 rm -f $HERE/lib_*.so
 build() { name=$1; shift; (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 "$@" -o $HERE/lib_$name.so $SRC); echo built $name; }
-build p32 -DENC_PIECE=32u
-build p64 -DENC_PIECE=64u
+build ov16 -DSUB_OV=16u
+build ov24 -DSUB_OV=24u

@@ -18,7 +18,7 @@ run() {
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench3) run bench3 600 python bench.py --config 3 --no-cpu-baseline ;;

@@ -3,7 +3,7 @@
 # MI355X_MICROARCH.md prescribes) over a short bench run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}; rm -rf $OUT; mkdir -p $OUT
 export TMPDIR=/tmp
 ARGS="${BENCH_ARGS:---no-cpu-baseline --steps 5 --warmup 2}"
 i=0
@@ -13,9 +13,9 @@ IFS=';' read -ra G <<< "$GROUPS_LIST"
 for g in "${G[@]}"; do
   i=$((i+1))
   echo "== pmc pass $i: $g"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${g//,/ } -d gpurun_out/pmc/p$i -o run \
-      --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${g//,/ } -d $OUT/p$i -o run \
+      --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?
-  echo "rc=$rc"; tail -n 2 gpurun_out/pmc/p$i.log
+  echo "rc=$rc"; tail -n 2 $OUT/p$i.log
   if [ $rc -ne 0 ]; then echo "stopping after pass $i"; exit $rc; fi
 done
