@@ -343,7 +343,8 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
                                                   uint32_t *__restrict__ tile_sums,
-                                                  uint16_t *__restrict__ piece_bits_out) {
+                                                  uint16_t *__restrict__ piece_bits_out,
+                                                  int bits_out) {
   __shared__ uint8_t lenT[256];
   __shared__ uint32_t sbits[ENC_WAVES][64];
   __shared__ uint32_t red[WG / 64];
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     __builtin_amdgcn_wave_barrier();
     if (sl) {
       e = (sbits[wv][lane] + 7u) >> 3;
-      if (out_len) out_len[t0 + lane] = e;
+      if (out_len) out_len[t0 + lane] = bits_out ? sbits[wv][lane] : e;
     }
   }
   if (tile_sums) {
@@ -387,179 +388,193 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
   }
 }
 
-// Pack: dst_off holds the encoded lengths on entry, the string offsets on
-// exit.  Each round's output -- contiguous, since pieces and strings are --
-// is assembled in the wave's LDS region with ds_or (pieces meet at
-// arbitrary bits) and stored with dwords; bytes shared with a neighbouring
-// wave or tile go bytewise, and a byte shared with the wave's previous
-// round is carried.
+// Pack (lib/nghttp2_hd_huffman.c:45-104), stream-parallel.  On entry
+// dst_off[s] holds string s's code bits (k_enc_count with bits_out); the
+// tile prologue turns them into byte offsets (E = ceil(bits / 8)).  A wave
+// owns 64 consecutive strings and walks their raw bytes as aligned 16-byte
+// chunks, 64 per round (one per lane), whatever the string lengths.
+//
+// Positions: with P(p) = code bits of the wave's bytes before byte p (a plain
+// prefix, no padding), byte p of string s starts at output bit
+// 8 * O_s + P(p) - P(a_s).  So a chunk's start = anchor[s] + P(chunk), with
+// anchor[s] = 8 * O_s - P(a_s) from one scan over the wave's strings and P
+// from one scan over the round's chunk sums.  Inside a chunk a string start
+// rounds the position up to a byte; the EOS-prefix padding itself
+// (:95-101) is OR'ed in afterwards by the string's own lane, which knows its
+// pad = 8 * E - bits.  Codes are appended MSB-first into a 64-bit register
+// and completed words OR'ed into the round's LDS image, which goes out as
+// whole dwords (zeroed behind the store); the partial word at a round's end
+// is carried into the next round, and the dwords at the wave's two ends go
+// bytewise.
+// ---------------------------------------------------------------------------
+#ifdef ENC_DBG
+__device__ uint32_t g_encdbg[64][8];
+extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__encdbg(void *out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_encdbg), sizeof(g_encdbg));
+}
+#endif
+#define ENC_RW 1024u  // LDS words per wave image: 1 KB of input at <= 30 bits a byte + edges
+
 __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_prefix,
-                                               const uint16_t *__restrict__ piece_bits_in) {
-  __shared__ uint2 codeT[256];
-  __shared__ uint8_t lenT[256];
-  __shared__ uint32_t region[ENC_WAVES][ENC_REGION / 4];
+                                               const uint32_t *__restrict__ tile_prefix) {
+  __shared__ uint2 codeT[257];                   // [256] = {0, 0}: bytes outside the wave
+  __shared__ uint32_t image[ENC_WAVES][ENC_RW];
+  __shared__ uint32_t heads[ENC_WAVES][36];
+  __shared__ uint32_t o_sh[WG + 1];
   __shared__ uint32_t red[WG / 64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
-  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+  if (threadIdx.x == 0) codeT[256] = make_uint2(0u, 0u);
+  lds_u32 *img = (lds_u32 *)image[wv];
+  for (uint32_t i = lane; i < ENC_RW; i += 64u) img[i] = 0u;
   const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
-  const uint32_t E_me = s_me < n ? dst_off[s_me] : 0u;
+  const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
+  const uint32_t E_me = (bits_me + 7u) >> 3;
+  // the wave's strings (lane = string) and its first chunk, before the tile scan
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
+  const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
+  const bool sl = lane < nstr;
+  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+  const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+  const uint32_t Z = nstr ? __builtin_amdgcn_readlane(b_l, nstr - 1u) : 0u;
+  const uint32_t c_end = (Z + 15u) >> 4;
+  uint4 wn = make_uint4(0, 0, 0, 0);  // the next round's chunk (prefetched)
+  if ((A >> 4) + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + (((A >> 4) + lane) << 4));
   uint32_t tot;
   const uint32_t o_me = tile_prefix[blockIdx.x] + block_excl_scan<WG>(E_me, red, &tot);  // (barrier)
   if (s_me < n) dst_off[s_me] = o_me;
-  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
-  if (t0 >= n) return;
-  lds_u32 *reg = (lds_u32 *)region[wv];
-  const uint32_t nstr = min(n - t0, 64u);
-  const bool sl = lane < nstr;
-  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
-  const uint32_t m_l = sl ? max(1u, (b_l - a_l + ENC_PIECE - 1u) / ENC_PIECE) : 0u;
-  const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
-  const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
-  uint32_t carry_bits = 0;              // bits of the string running into this round
-  uint64_t carry_byte_at = ~0ull;       // global index of a byte shared with the previous round
-  uint32_t carry_byte = 0;
-  for (uint32_t r0 = 0; r0 < M;) {
-    const uint32_t q = r0 + lane;
-    const bool live = q < M;
-    const EncPiece p = enc_piece(q, nstr, P_l, X_l, a_l, b_l);
-    PieceBytes pb;
-    pb.load(src, p, live);
-    const uint32_t jmax = wave_max(pb.len);
-    uint32_t pbits;
-    if (piece_bits_in) {  // from the count pass
-      pbits = live ? piece_bits_in[enc_piece_slot(p.a - off[0], t0 + p.i, p.k)] : 0u;
-    } else {
-      pbits = live ? piece_bits(pb, lenT, jmax) : 0u;
-    }
-    // bit offset of the piece in its string: segmented exclusive scan over
-    // lanes (segments start at k = 0), the first segment continues the carry
-    uint32_t ps = pbits;
-    int32_t hm = (!live || p.k == 0) ? (int32_t)lane : -1;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t o2 = __shfl_up(ps, d, 64);
-      const int32_t oh = __shfl_up(hm, d, 64);
-      if (lane >= d) {
-        ps += o2;
-        hm = max(hm, oh);
-      }
-    }
-    const uint32_t excl_h = __shfl(ps - pbits, hm >= 0 ? (uint32_t)hm : 0u, 64);
-    const uint32_t poff = (hm >= 0 ? ps - excl_h : ps + carry_bits) - pbits;
-    const uint32_t tbits = poff + pbits;                      // string bits through this piece
-    const uint32_t pad = p.last ? ((8u - (tbits & 7u)) & 7u) : 0u;
-    const uint64_t ostr = (uint64_t)__shfl(o_me, p.i, 64);   // o of wave string p.i (lane p.i)
-    const uint64_t gbit = 8ull * ostr + poff;                 // first output bit of the piece
-    const uint64_t gend = gbit + pbits + pad;
-    // round size: as many pieces as fit the region
-    const uint64_t B0 = __builtin_amdgcn_readlane((uint32_t)(gbit >> 3), 0) |
-                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(gbit >> 35), 0) << 32);
-    const uint64_t D0 = B0 & ~3ull;
-    const bool fits = live && ((gend + 7u) >> 3) - D0 + 8u <= ENC_REGION;
-    const uint64_t fitmask = __ballot(fits);
-    const uint32_t nv = ~fitmask ? (uint32_t)__builtin_ctzll(~fitmask) : 64u;  // leading lanes that fit (>= 1)
-    const bool act = lane < nv;
-    const uint32_t lastl = nv - 1u;
-    const uint64_t B1 = (uint64_t)__builtin_amdgcn_readlane((uint32_t)((gend + 7u) >> 3), lastl) |
-                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(((gend + 7u) >> 3) >> 32), lastl) << 32);
-    // zero the region's words, then OR every piece's bits in
-    const uint32_t ndw = (uint32_t)((B1 - D0 + 3u) >> 2);
-    for (uint32_t x = lane; x <= ndw; x += 64u) reg[x] = 0u;
+  o_sh[threadIdx.x] = o_me;
+  if (threadIdx.x == WG - 1) o_sh[WG] = o_me + E_me;
+  __syncthreads();
+  if (nstr == 0) return;
+  const uint32_t OA = o_sh[64u * wv], OZ = o_sh[64u * wv + nstr];  // the wave's output bytes
+  const uint64_t G0 = 8ull * OA;
+  // anchor[s] = 8 (O_s - OA) - P(a_s)   (positions relative to G0)
+  const uint32_t P_a = wave_incl_scan(sl ? bits_me : 0u) - (sl ? bits_me : 0u);
+  const uint32_t anchor_l = 8u * (o_me - OA) - P_a;
+  const uint32_t pad_l = sl ? 8u * E_me - bits_me : 0u;  // EOS-prefix bits after string l
+  const uint32_t olast_l = o_me + E_me - 1u;             // its last output byte (if E > 0)
+  lds_u32 *hb = (lds_u32 *)heads[wv];
+  uint32_t Pc = 0;     // P at the round's first byte
+  uint32_t x = 0;      // output bit at the round's start (relative to G0)
+  for (uint32_t cb = A >> 4; cb < c_end; cb += 64u) {
+    const bool last_round = cb + 64u >= c_end;
+    const uint32_t base = cb << 4;
+    const uint64_t WB = (G0 + x) >> 5;  // global word of img[0]
+    // ---- string starts in this round (alignment points)
+    if (lane < 33u) hb[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // Big-endian region words.  A piece's first and last words may hold
-    // neighbouring pieces' bits: ORed in at the end (LDS atomics).  Its
-    // interior words are its own: each is stored when it completes.  The
-    // EOS-prefix padding of a string's last piece is the code at index len.
-    if (act && gend > gbit) {
-      const uint32_t rb0 = (uint32_t)(gbit - 8ull * D0);      // region-relative bits
-      const uint32_t rbe = (uint32_t)(gend - 8ull * D0);
-      const uint32_t w0 = rb0 >> 5, wl = (rbe - 1u) >> 5;     // first and last word
-      uint32_t rb = rb0, cw = 0, first_val = 0, last_val = 0;
-      const uint32_t padcode = pad ? (~0u) << (32u - pad) : 0u;
-      // one step: append a code of len bits at rb
-#define ENC_STEP(CODE, LEN)                                                      \
-      do {                                                                     \
-        const uint32_t code_ = (CODE), len_ = (LEN);                           \
-        const uint32_t o_ = rb & 31u;                                          \
-        const uint64_t v_ = ((uint64_t)code_ << 32) >> o_;                     \
-        cw |= (uint32_t)(v_ >> 32);                                            \
-        if (o_ + len_ >= 32u) { /* word rb >> 5 complete */                    \
-          const uint32_t wd_ = rb >> 5;                                        \
-          if (wd_ != w0 && wd_ != wl) reg[wd_] = cw;                           \
-          first_val = wd_ == w0 ? cw : first_val;                              \
-          last_val = (wd_ == wl && wd_ != w0) ? cw : last_val;                 \
-          cw = (uint32_t)v_;                                                   \
-        }                                                                      \
-        rb += len_;                                                            \
-      } while (0)
+    if (sl && a_l < b_l && a_l >= base && a_l - base < 1024u)
+      atomicOr((uint32_t *)&hb[(a_l - base) >> 5], 1u << ((a_l - base) & 31u));
+    const uint32_t p0 = base + 16u * lane;  // my chunk's first byte
+    const uint32_t lo = A > p0 ? min(A - p0, 16u) : 0u;
+    const uint32_t hi = Z > p0 ? min(Z - p0, 16u) : 0u;
+    const uint32_t vm = hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
+    if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + p0 + 1024u);
+    uint2 cc[16];
+    uint32_t S = 0;
 #pragma unroll
-      for (int k = 0; k < ENC_PW; ++k) {
-        if ((uint32_t)(4 * k) <= jmax) {  // uniform
-          const uint32_t wd = pb.w[k];
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t b = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      cc[j] = codeT[((vm >> j) & 1u) ? b : 256u];
+    }
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const uint32_t j = 4 * k + b;
-            const uint2 c = codeT[(wd >> (8 * b)) & 0xFFu];
-            const bool in = j < pb.len;
-            ENC_STEP(in ? c.x : (j == pb.len ? padcode : 0u), in ? c.y : (j == pb.len ? pad : 0u));
-          }
+    for (int j = 0; j < 16; ++j) S += cc[j].y;
+    // ---- my chunk's start: anchor of the string holding its first valid
+    // byte, plus P there
+    const uint32_t Sinc = wave_incl_scan(S);
+    const uint32_t Pme = Pc + Sinc - S;
+    const uint32_t q = p0 + lo;  // my first valid byte (A - p0 < 16 when A > p0)
+    uint32_t lo_i = 0, hi_i = nstr;
+#pragma unroll
+    for (int st = 0; st < 7; ++st) {
+      const uint32_t mid = (lo_i + hi_i) >> 1;
+      const uint32_t am = __shfl(a_l, min(mid, 63u), 64);
+      if (lo_i < hi_i) {
+        if (am <= q) lo_i = mid + 1u; else hi_i = mid;
+      }
+    }
+    const uint32_t sidx = lo_i ? lo_i - 1u : 0u;
+    const uint32_t start = __shfl(anchor_l, sidx, 64) + Pme;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t hm = (hb[lane >> 1] >> (16u * (lane & 1u))) & vm & 0xFFFFu;
+#ifdef ENC_DBG
+    if (blockIdx.x == 0 && wv == 0 && cb == (A >> 4)) {
+      g_encdbg[lane][0] = start; g_encdbg[lane][1] = sidx; g_encdbg[lane][2] = S; g_encdbg[lane][3] = Pme;
+      g_encdbg[lane][4] = hm; g_encdbg[lane][5] = vm; g_encdbg[lane][6] = anchor_l; g_encdbg[lane][7] = bits_me;
+    }
+#endif
+    // ---- emit
+    uint32_t endp = start;
+    if (vm) {
+      const uint64_t gp = G0 + start;
+      uint32_t wa = (uint32_t)((gp >> 5) - WB);  // image word
+      uint32_t nacc = (uint32_t)gp & 31u;
+      uint64_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t h7 = ((hm >> j) & 1u) ? 7u : 0u;
+        nacc = (nacc + h7) & ~h7;  // a string starts: next byte boundary
+        acc |= ((uint64_t)cc[j].x << 32) >> nacc;
+        nacc += cc[j].y;
+        if (nacc >= 32u) {
+          atomicOr((uint32_t *)&img[wa], (uint32_t)(acc >> 32));
+          ++wa;
+          acc <<= 32;
+          nacc -= 32u;
         }
       }
-      if (pb.len == ENC_PIECE) ENC_STEP(padcode, pad);  // padding after a full piece
-#undef ENC_STEP
-      if (rbe & 31u) {  // the final word did not complete: cw holds its bits
-        if (wl == w0) first_val = cw; else last_val = cw;
-      }
-      atomicOr((uint32_t *)&reg[w0], first_val);
-      if (wl != w0) atomicOr((uint32_t *)&reg[wl], last_val);
+      if (nacc) atomicOr((uint32_t *)&img[wa], (uint32_t)(acc >> 32));
+      endp = (uint32_t)(32ull * (WB + wa) + nacc - G0);
+    }
+    // end of the round: the last lane with input
+    const uint64_t live = __ballot(vm != 0);
+    uint32_t xe = live ? __builtin_amdgcn_readlane(endp, 63u - __builtin_clzll(live)) : x;
+    if (last_round) xe = 8u * (OZ - OA);
+    const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
+    // ---- EOS-prefix padding of the strings that end in this round
+    if (sl && pad_l && b_l - 1u >= base && b_l - 1u - base < 1024u && b_l > a_l) {
+      const uint32_t r = (uint32_t)((olast_l >> 2) - WB);
+      atomicOr((uint32_t *)&img[r], ((1u << pad_l) - 1u) << (24u - 8u * (olast_l & 3u)));
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // words to bytes (little-endian memory order)
-    for (uint32_t x = lane; x < ndw; x += 64u) reg[x] = __builtin_bswap32(reg[x]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // a byte shared with the previous round: merge its bits
-    if (lane == 0 && carry_byte_at == B0) {
-      lds_u8 *rb8 = (lds_u8 *)reg;
-      rb8[B0 - D0] |= (uint8_t)carry_byte;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // store [B0, B1): whole dwords, bytewise at the two ends
-    {
-      const lds_u8 *rb8 = (const lds_u8 *)reg;
-      for (uint32_t x = lane; x < ndw; x += 64u) {
-        const uint64_t ga = D0 + 4ull * x;
-        if (ga >= B0 && ga + 4u <= B1 && ga + 4u <= dst_cap) {
-          *reinterpret_cast<uint32_t *>(dst + ga) = reg[x];
-        } else {
-          for (uint32_t y = 0; y < 4; ++y) {
-            const uint64_t gq = ga + y;
-            if (gq >= B0 && gq < B1 && gq < dst_cap) dst[gq] = rb8[4u * x + y];
-          }
+    // ---- store whole words and zero them; carry a partial last word
+    const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
+    for (uint32_t i = lane; i < nst; i += 64u) {
+      const uint32_t v = __builtin_bswap32(img[i]);
+      img[i] = 0u;
+      const uint64_t ga = 4ull * (WB + i);
+      if (ga >= OA && ga + 4u <= OZ && ga + 4u <= dst_cap) {
+        *reinterpret_cast<uint32_t *>(dst + ga) = v;
+      } else {
+        for (uint32_t y = 0; y < 4u; ++y) {
+          const uint64_t gq = ga + y;
+          if (gq >= OA && gq < OZ && gq < dst_cap) dst[gq] = (uint8_t)(v >> (8u * y));
         }
       }
     }
-    // carry: the string running past this round, and its last partial byte
-    const uint32_t tb_last = __builtin_amdgcn_readlane(tbits, lastl);
-    const bool last_last = __builtin_amdgcn_readlane(p.last ? 1u : 0u, lastl) != 0u;
-    carry_bits = last_last ? 0u : tb_last;
-    if (!last_last && (tb_last & 7u)) {
-      carry_byte_at = B1 - 1u;
-      carry_byte = ((const lds_u8 *)reg)[B1 - 1u - D0];
-    } else {
-      carry_byte_at = ~0ull;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (!last_round && nst < nw) {  // the partial word moves to img[0]
+      const uint32_t cw = img[nst];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        img[nst] = 0u;
+        img[0] = cw;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    r0 += nv;
+    Pc += __builtin_amdgcn_readlane(Sinc, 63);
+    x = xe;
   }
 }
 
@@ -1300,7 +1315,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
-                     src_off, n, enc_len, (uint32_t *)nullptr, (uint16_t *)nullptr);
+                     src_off, n, enc_len, (uint32_t *)nullptr, (uint16_t *)nullptr, 0);
   return hip_rv(hipGetLastError());
 }
 
@@ -1316,19 +1331,11 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  // Per-piece bit counts (count pass -> pack pass) when the workspace holds
-  // them for the largest raw size dst_cap admits (dst_cap >= encode_bound).
-  uint16_t *pbits = nullptr;
-  const size_t tiles_bytes = nghttp2_amd_hd_huff_workspace_size(n);
-  if (workspace_size > tiles_bytes && dst_cap > (size_t)n + 16u) {
-    const uint64_t raw_max = ((uint64_t)(dst_cap - n - 16u) * 8u) / 30u + 16u;
-    const uint64_t need = (raw_max / ENC_PIECE + n + 1u) * sizeof(uint16_t);
-    if (workspace_size - tiles_bytes >= need) pbits = (uint16_t *)((char *)workspace + tiles_bytes);
-  }
-  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, pbits);
+  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles,
+                     (uint16_t *)nullptr, 1);
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
   hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, (const uint16_t *)pbits);
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
 }
 
