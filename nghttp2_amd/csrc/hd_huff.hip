@@ -87,14 +87,37 @@ __device__ unsigned long long g_stamps[4096][16];
 // ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
+// Wave-wide inclusive scans on DPP (row shifts within 16-lane rows, then
+// row broadcasts of lanes 15 and 31): VALU only, no LDS round trips.
+// Lanes whose DPP source lies outside the row read 0, the identity of
+// add / max / or over unsigned values.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+#define WAVE_SCAN(v, OP)                                                        \
+  do {                                                                          \
+    v = OP(v, dpp0<0x111>(v));                                                  \
+    v = OP(v, dpp0<0x112>(v));                                                  \
+    v = OP(v, dpp0<0x114>(v));                                                  \
+    v = OP(v, dpp0<0x118>(v));                                                  \
+    v = OP(v, dpp0<0x142, 0xa>(v));                                             \
+    v = OP(v, dpp0<0x143, 0xc>(v));                                             \
+  } while (0)
+__device__ __forceinline__ uint32_t op_add(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t op_max(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t op_or(uint32_t a, uint32_t b) { return a | b; }
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
+  WAVE_SCAN(v, op_add);
   return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  WAVE_SCAN(v, op_max);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {  // uniform result
+  WAVE_SCAN(v, op_or);
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
 // Exclusive scan across a workgroup of NT threads (NT/64 words of `sm`).
@@ -407,12 +430,6 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
 // is carried into the next round, and the dwords at the wave's two ends go
 // bytewise.
 // ---------------------------------------------------------------------------
-#ifdef ENC_DBG
-__device__ uint32_t g_encdbg[64][8];
-extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__encdbg(void *out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_encdbg), sizeof(g_encdbg));
-}
-#endif
 #define ENC_RW 1024u  // LDS words per wave image: 1 KB of input at <= 30 bits a byte + edges
 
 __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
@@ -420,14 +437,15 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
                                                const uint32_t *__restrict__ tile_prefix) {
-  __shared__ uint2 codeT[257];                   // [256] = {0, 0}: bytes outside the wave
+  __shared__ uint2 codeT[512];                   // [256..511] = {0, 0}: bytes outside the wave
   __shared__ uint32_t image[ENC_WAVES][ENC_RW];
   __shared__ uint32_t heads[ENC_WAVES][36];
+  __shared__ uint32_t cand[ENC_WAVES][65];
   __shared__ uint32_t o_sh[WG + 1];
   __shared__ uint32_t red[WG / 64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
-  if (threadIdx.x == 0) codeT[256] = make_uint2(0u, 0u);
+  codeT[256 + threadIdx.x] = make_uint2(0u, 0u);
   lds_u32 *img = (lds_u32 *)image[wv];
   for (uint32_t i = lane; i < ENC_RW; i += 64u) img[i] = 0u;
   const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
@@ -458,7 +476,9 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
   const uint32_t pad_l = sl ? 8u * E_me - bits_me : 0u;  // EOS-prefix bits after string l
   const uint32_t olast_l = o_me + E_me - 1u;             // its last output byte (if E > 0)
   lds_u32 *hb = (lds_u32 *)heads[wv];
+  lds_u32 *cd = (lds_u32 *)cand[wv];
   uint32_t Pc = 0;     // P at the round's first byte
+  uint32_t scarry = 0; // 1 + the string running into the round
   uint32_t x = 0;      // output bit at the round's start (relative to G0)
   for (uint32_t cb = A >> 4; cb < c_end; cb += 64u) {
     const bool last_round = cb + 64u >= c_end;
@@ -466,50 +486,48 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
     const uint64_t WB = (G0 + x) >> 5;  // global word of img[0]
     // ---- string starts in this round (alignment points)
     if (lane < 33u) hb[lane] = 0u;
+    cd[lane] = 0u;
+    if (lane == 0) cd[64] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (sl && a_l < b_l && a_l >= base && a_l - base < 1024u)
+    // a string starting in this round: its head bit, and it holds the first
+    // valid byte of every chunk from kf on (chunk 0 of the first round starts
+    // at A itself)
+    if (sl && a_l < b_l && a_l >= base && a_l - base < 1024u) {
       atomicOr((uint32_t *)&hb[(a_l - base) >> 5], 1u << ((a_l - base) & 31u));
+      const uint32_t kf = a_l <= max(base, A) ? 0u : (a_l - base + 15u) >> 4;
+      atomicMax((uint32_t *)&cd[kf], lane + 1u);
+    }
     const uint32_t p0 = base + 16u * lane;  // my chunk's first byte
     const uint32_t lo = A > p0 ? min(A - p0, 16u) : 0u;
     const uint32_t hi = Z > p0 ? min(Z - p0, 16u) : 0u;
     const uint32_t vm = hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    const uint32_t iv = ~vm << 11;  // bit 11 + j: byte j is outside the wave -> zero entry
     const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
     if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + p0 + 1024u);
     uint2 cc[16];
-    uint32_t S = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint32_t b = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      cc[j] = codeT[((vm >> j) & 1u) ? b : 256u];
+      const uint32_t b8 = (j & 3) ? (wd[j >> 2] >> (8 * (j & 3) - 3)) & 0x7F8u : (wd[j >> 2] << 3) & 0x7F8u;
+      cc[j] = *(const uint2 *)((const char *)codeT + (b8 | ((iv >> j) & 0x800u)));
     }
+    uint32_t S = 0, Lmax = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) S += cc[j].y;
+    for (int j = 0; j < 16; ++j) {
+      S += cc[j].y;
+      Lmax = max(Lmax, cc[j].y);
+    }
     // ---- my chunk's start: anchor of the string holding its first valid
-    // byte, plus P there
+    // byte (an inclusive max-scan of the start marks), plus P there
     const uint32_t Sinc = wave_incl_scan(S);
     const uint32_t Pme = Pc + Sinc - S;
-    const uint32_t q = p0 + lo;  // my first valid byte (A - p0 < 16 when A > p0)
-    uint32_t lo_i = 0, hi_i = nstr;
-#pragma unroll
-    for (int st = 0; st < 7; ++st) {
-      const uint32_t mid = (lo_i + hi_i) >> 1;
-      const uint32_t am = __shfl(a_l, min(mid, 63u), 64);
-      if (lo_i < hi_i) {
-        if (am <= q) lo_i = mid + 1u; else hi_i = mid;
-      }
-    }
-    const uint32_t sidx = lo_i ? lo_i - 1u : 0u;
-    const uint32_t start = __shfl(anchor_l, sidx, 64) + Pme;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    const uint32_t sm = wave_incl_max(max(cd[lane], scarry));
+    const uint32_t start = __shfl(anchor_l, sm - 1u, 64) + Pme;
     const uint32_t hm = (hb[lane >> 1] >> (16u * (lane & 1u))) & vm & 0xFFFFu;
-#ifdef ENC_DBG
-    if (blockIdx.x == 0 && wv == 0 && cb == (A >> 4)) {
-      g_encdbg[lane][0] = start; g_encdbg[lane][1] = sidx; g_encdbg[lane][2] = S; g_encdbg[lane][3] = Pme;
-      g_encdbg[lane][4] = hm; g_encdbg[lane][5] = vm; g_encdbg[lane][6] = anchor_l; g_encdbg[lane][7] = bits_me;
-    }
-#endif
+    const uint32_t hmw = wave_or(hm);  // heads at each byte position, over the wave
+    const bool short_codes = __ballot(Lmax > 16u) == 0;
     // ---- emit
     uint32_t endp = start;
     if (vm) {
@@ -517,19 +535,43 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
       uint32_t wa = (uint32_t)((gp >> 5) - WB);  // image word
       uint32_t nacc = (uint32_t)gp & 31u;
       uint64_t acc = 0;
+#define ENC_ALIGN(J)                                                     \
+      if (hmw & (1u << (J))) {  /* some lane starts a string here */     \
+        const uint32_t h7 = ((hm >> (J)) & 1u) ? 7u : 0u;                 \
+        nacc = (nacc + h7) & ~h7;  /* next byte boundary */               \
+      }
+#define ENC_APPEND(J)                                                    \
+      acc |= ((uint64_t)cc[J].x << 32) >> nacc;                          \
+      nacc += cc[J].y;
+#define ENC_FLUSH()                                                      \
+      if (nacc >= 32u) {                                                 \
+        atomicOr((uint32_t *)&img[wa], (uint32_t)(acc >> 32));           \
+        ++wa;                                                            \
+        acc <<= 32;                                                      \
+        nacc -= 32u;                                                     \
+      }
+      if (short_codes) {
+        // every code <= 16 bits: nacc <= 32 on entry to a pair, <= 64 after
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t h7 = ((hm >> j) & 1u) ? 7u : 0u;
-        nacc = (nacc + h7) & ~h7;  // a string starts: next byte boundary
-        acc |= ((uint64_t)cc[j].x << 32) >> nacc;
-        nacc += cc[j].y;
-        if (nacc >= 32u) {
-          atomicOr((uint32_t *)&img[wa], (uint32_t)(acc >> 32));
-          ++wa;
-          acc <<= 32;
-          nacc -= 32u;
+        for (int j = 0; j < 16; j += 2) {
+          ENC_ALIGN(j);
+          ENC_APPEND(j);
+          ENC_ALIGN(j + 1);
+          ENC_APPEND(j + 1);
+          ENC_FLUSH();
+        }
+        ENC_FLUSH();
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          ENC_ALIGN(j);
+          ENC_APPEND(j);
+          ENC_FLUSH();
         }
       }
+#undef ENC_ALIGN
+#undef ENC_APPEND
+#undef ENC_FLUSH
       if (nacc) atomicOr((uint32_t *)&img[wa], (uint32_t)(acc >> 32));
       endp = (uint32_t)(32ull * (WB + wa) + nacc - G0);
     }
@@ -574,6 +616,7 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     Pc += __builtin_amdgcn_readlane(Sinc, 63);
+    scarry = max(__builtin_amdgcn_readlane(sm, 63), cd[64]);
     x = xe;
   }
 }
