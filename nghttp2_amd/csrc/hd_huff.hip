@@ -55,28 +55,31 @@ namespace host {
 #define HD_DIAG_STAMPS 0   // diagnostic build only: per-phase s_memtime sums
 #endif
 #if HD_DIAG_STAMPS
-// [wg][slot]: per-phase cycles (slots 0..7, accumulated in registers of
-// thread 0 and stored once), 8 verify iterations, 9 mismatches, 10 rounds,
-// 11 tiles, 12..14 wave loop trips (fast, checked, warm-up)
+// Diagnostic build only: per-wave phase cycles of k_decode (s_memtime deltas
+// kept in SGPRs, one row per wave written once at exit).  Slots: 0 task
+// setup, 1 staging, 2 pass 1, 3 verify, 4 scan, 5 pass 2, 6 round end,
+// 7 lifetime, 8 tasks, 9 rounds.
 __device__ unsigned long long g_stamps[4096][16];
-#define STAMP(slot, t0)                                                        \
+#define WSTAMP(slot)                                                           \
   do {                                                                         \
-    __syncthreads();                                                           \
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime();               \
-    stamp_acc[slot] += t1_ - (t0);                                             \
-    (t0) = t1_;                                                                \
+    wst[slot] += t1_ - wt0;                                                    \
+    wt0 = t1_;                                                                 \
   } while (0)
-#define COUNT(slot, v) do { if (threadIdx.x == 0) stamp_acc[slot] += (v); } while (0)
-#define STAMP_FLUSH()                                                          \
+#define WCOUNT(slot) (++wst[slot])
+#define WSTAMP_INIT() unsigned long long wst[10] = {}, wt0 = __builtin_amdgcn_s_memtime(), wbirth = wt0
+#define WSTAMP_FLUSH()                                                         \
   do {                                                                         \
-    if (threadIdx.x == 0)                                                      \
-      for (int s_ = 0; s_ < 12; ++s_) g_stamps[blockIdx.x & 4095][s_] += stamp_acc[s_]; \
+    wst[7] = __builtin_amdgcn_s_memtime() - wbirth;                            \
+    if (lane == 0)                                                             \
+      for (int s_ = 0; s_ < 10; ++s_) g_stamps[(blockIdx.x * DEC_WAVES + wv) & 4095][s_] = wst[s_]; \
   } while (0)
 #define DCTR(k) (++dctr[k])
 #else
-#define STAMP(slot, t0) do { } while (0)
-#define COUNT(slot, v) do { } while (0)
-#define STAMP_FLUSH() do { } while (0)
+#define WSTAMP(slot) do { } while (0)
+#define WCOUNT(slot) do { } while (0)
+#define WSTAMP_INIT() do { } while (0)
+#define WSTAMP_FLUSH() do { } while (0)
 #define DCTR(k) do { } while (0)
 #endif
 
@@ -624,9 +627,16 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
 // ---------------------------------------------------------------------------
 // decode: canonical multi-symbol decoder
 // ---------------------------------------------------------------------------
-#define NLONG 14  // code lengths > HD_HUFF_LUT_BITS (13,14,15,19..28,30)
+#define HD_COUNT_ROW(LEN, LIM, FIRST, BASE) +1
+enum { NLONG = 0 HD_HUFF_LONG_CODES(HD_COUNT_ROW) };  // code lengths > HD_HUFF_LUT_BITS
+#undef HD_COUNT_ROW
 
 #define NLONG_PAD 16  // search width (padding rows repeat the last row)
+static_assert(NLONG <= NLONG_PAD, "long-code search too narrow");
+// Lookup entry (tools/gen_tables.py): sym1 | sym2 << 8 | L1 << 16 | cnt << 21 | used << 27
+#define E_L1(e) (((e) >> 16) & 31u)
+#define E_CNT(e) (((e) >> 21) & 3u)
+#define E_USED(e) ((e) >> 27)
 struct DecTables {
   uint32_t lut[1 << HD_HUFF_LUT_BITS];
   uint32_t lut2[64];               // 13..16-bit codes (second level)
@@ -686,7 +696,9 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
 // symbol count (a segmented scan across lanes).
 // ---------------------------------------------------------------------------
 #define WAVE 64
-#define DEC_WAVES 8                                // waves per decode workgroup (one table copy)
+#ifndef DEC_WAVES
+#define DEC_WAVES 16  // waves per decode workgroup: one 64 KB lookup per CU
+#endif
 #define DEC_NT (WAVE * DEC_WAVES)
 #define TASK_STR 64                                // strings per wave task
 #define PIECE_BYTES 64u                            // input bytes per item (string piece)
@@ -714,17 +726,17 @@ __device__ __forceinline__ uint32_t win_q(const lds_u32 *ibe, uint32_t q) {  // 
 }
 __device__ __forceinline__ uint32_t win_at(const lds_u32 *ibe, uint32_t bp) { return win_q(ibe, bp - 1u); }
 
-// Decode output sinks.  put2(e, cnt) appends the cnt (1..2) symbols of a
-// table entry: sym1 in bits 0..7, sym2 in bits 16..23.  Output goes straight
+// Decode output sinks.  put2(v, cnt) appends cnt (1..2) symbols: sym1 in
+// bits 0..7 of v, sym2 in bits 8..15 (zero when cnt = 1).  Output goes straight
 // to global memory: DwordSink for items that start an engine slot (dword
 // aligned), GlobalSink (bytes) for pieces that continue a string, whose
 // first byte shares a dword with the previous piece (another lane).
 struct GlobalSink {
   uint8_t *p;
   __device__ __forceinline__ uint32_t count() const { return (uint32_t)(uintptr_t)p; }
-  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
-    p[0] = (uint8_t)e;
-    if (cnt > 1) p[1] = (uint8_t)(e >> 16);
+  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
+    p[0] = (uint8_t)v;
+    if (cnt > 1) p[1] = (uint8_t)(v >> 8);
     p += cnt;
   }
 };
@@ -743,8 +755,7 @@ struct DwordSink {
     na = n = 0;
   }
   __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
-    const uint32_t v = (e & 0xFFu) | ((e >> 8) & 0xFF00u);
+  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
     acc |= (uint64_t)v << (8u * na);
     na += cnt;
     n += cnt;
@@ -780,8 +791,7 @@ struct UDwordSink {
     n = 0;
   }
   __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
-    const uint32_t v = (e & 0xFFu) | ((e >> 8) & 0xFF00u);
+  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
     acc |= (uint64_t)v << (8u * na);
     na += cnt;
     n += cnt;
@@ -820,10 +830,10 @@ struct CheckedSink {
   bool ovf;
   __device__ __forceinline__ void init(uint8_t *q, uint32_t c) { p = q; cap = c; n = 0; ovf = false; }
   __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t e, uint32_t cnt) {
-    if (n < cap) p[n] = (uint8_t)e; else ovf = true;
+  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
+    if (n < cap) p[n] = (uint8_t)v; else ovf = true;
     if (cnt > 1) {
-      if (n + 1 < cap) p[n + 1] = (uint8_t)(e >> 16); else ovf = true;
+      if (n + 1 < cap) p[n + 1] = (uint8_t)(v >> 8); else ovf = true;
     }
     n += cnt;
   }
@@ -842,7 +852,7 @@ __device__ __forceinline__ uint32_t long_entry(const DecTables &T, uint32_t win,
   const uint32_t L = T.long_len[i];
   const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
   if (L <= rem && sym == 256) return 0xFFFFFFFFu;
-  return (L <= rem ? sym : 0u) | (L << 8) | (1u << 24) | (L << 27);
+  return (L <= rem ? sym : 0u) | (L << 16) | (1u << 21) | (L << 27);
 }
 
 // First-level miss: the 13..16-bit second level, else the search.
@@ -879,10 +889,10 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
         r.entry = r.exit = XUNKNOWN;
         return r;
       }
-      const uint32_t L1 = (e >> 8) & 31u, L2 = (e >> 13) & 7u;
+      const uint32_t L1 = E_L1(e), U = E_USED(e);
       if (L1 > rem) break;  // reached the string's tail
-      const bool two = L2 != 0 && bp + L1 < bseg && L1 + L2 <= rem;
-      bp += two ? L1 + L2 : L1;
+      const bool two = E_CNT(e) == 2u && bp + L1 < bseg && U <= rem;
+      bp += two ? U : L1;
     }
   }
   r.entry = bp;
@@ -911,8 +921,8 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
           e = 0u;
         }
       }
-      sink.put2(e, (e >> 24) & 3u);
-      const uint32_t used = e >> 27;
+      sink.put2(e & 0xFFFFu, E_CNT(e));
+      const uint32_t used = E_USED(e);
       bp += used;
       bb <<= used;
       nb -= used;
@@ -928,8 +938,16 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
   uint32_t q = bp - 1u;
   while ((int32_t)q < F) {
     DCTR(0);
+#if HD_ABL_NOWIN  // timing ablation only (wrong output): no window read
+    const uint32_t w = q * 0x9E3779B9u;
+#else
     const uint32_t w = win_q(ibe, q);
+#endif
+#if HD_ABL_NOLUT  // timing ablation only (wrong output): no lookup read
+    uint32_t e = (8u << 27) | (2u << 21) | (w >> 16);
+#else
     uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
+#endif
     if (e == 0u) {
       e = slow_entry(T, w, 30u);
       if (e == 0xFFFFFFFFu) {
@@ -937,8 +955,10 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
         e = 0u;
       }
     }
-    sink.put2(e, (e >> 24) & 3u);
-    q += e >> 27;
+#if !HD_ABL_NOSINK  // timing ablation only (wrong output): no output
+    sink.put2(e & 0xFFFFu, E_CNT(e));
+#endif
+    q += E_USED(e);
   }
   bp = q + 1u;
 #endif
@@ -957,17 +977,16 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
         break;
       }
     }
-    const uint32_t L1 = (e >> 8) & 31u;
-    const uint32_t L2 = (e >> 13) & 7u;
+    const uint32_t L1 = E_L1(e), U = E_USED(e);
     if (L1 > rem) {  // the tail is a proper prefix of a code
       r.at_end = true;
       r.t = rem;
       r.win = w;
       break;
     }
-    const bool two = L2 != 0 && L1 + L2 <= rem && bp + L1 < bstop;
-    sink.put2(e, two ? 2u : 1u);
-    bp += two ? L1 + L2 : L1;
+    const bool two = E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
+    sink.put2(two ? e & 0xFFFFu : e & 0xFFu, two ? 2u : 1u);
+    bp += two ? U : L1;
   }
   if (!failed && bp == bend) r.at_end = true;
   r.exit = failed ? XFAIL : bp;
@@ -1036,6 +1055,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
   lds_u32 *ibw = (lds_u32 *)S.ibe[wv];
   const lds_u32 *ibe = ibw;
   stage_dec_tables(S.T, DEC_NT);  // the kernel's only workgroup barrier
+  WSTAMP_INIT();
   const uint32_t off0 = off[0];
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
   uint32_t dctr[3] = {0, 0, 0};
@@ -1043,6 +1063,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
   for (uint32_t task = blockIdx.x * DEC_WAVES + wv; task < ntask; task += gridDim.x * DEC_WAVES) {
     const uint32_t t0 = task * TASK_STR;
     const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
+    WCOUNT(8);
     // lane l: task string l
     const bool sl = lane < nstr;
     const uint32_t a_l = sl ? off[t0 + lane] : 0u;
@@ -1077,6 +1098,8 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
         it.s = it.a + PIECE_BYTES * it.k;
         it.last = it.s + PIECE_BYTES >= it.b;
       }
+      WCOUNT(9);
+      WSTAMP(0);
       // ---- stage the round's input: [first item (- warm-up), last item's reach)
       const uint32_t A = __builtin_amdgcn_readlane(it.k ? it.s - SUB_OV : it.s, 0);
       const uint32_t Z = __builtin_amdgcn_readlane(min(it.b, it.s + PIECE_BYTES), nv - 1u) + 12u;
@@ -1096,6 +1119,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
+      WSTAMP(1);
       // the carried exit is a bit position of the previous round's staging
       if (carry_exit < NOSPEC) carry_exit -= 8u * (IB - IB_prev);
       IB_prev = IB;
@@ -1148,6 +1172,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
           r = decode_item<true>(S.T, ibe, bseg - 8u * SUB_OV, bseg, bstop, bend, nk, dctr);
         }
       }
+      WSTAMP(2);
       // ---- verify / redo (wave): the entry of item (i, k > 0) must equal
       // the exit of the previous lane's item (i, k - 1), or the carry.  A
       // mismatched item is re-decoded once its predecessor is settled (not
@@ -1169,6 +1194,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
           }
         }
       }
+      WSTAMP(3);
       // ---- symbols of each string through each item: segmented inclusive
       // scan over lanes, segments headed by k = 0 items; the first segment
       // continues the carry
@@ -1186,6 +1212,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
       }
       const uint32_t excl_h = __shfl(ps - v, hm >= 0 ? (uint32_t)hm : 0u, 64);
       const uint32_t seg = hm >= 0 ? ps - excl_h : ps + carry_cnt;
+      WSTAMP(4);
       // ---- pass 2: k > 0 exact, at the string's running symbol count
       if (valid && it.k > 0) {
         const uint32_t soff = seg - r.cnt;
@@ -1218,6 +1245,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
           if (flags_out) flags_out[j] = (uint8_t)fl;
         }
       }
+      WSTAMP(5);
       // ---- carry the string running into the next round
       carry_exit = __builtin_amdgcn_readlane(r.exit, nv - 1u);
       carry_cnt = __builtin_amdgcn_readlane(seg, nv - 1u);
@@ -1225,8 +1253,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      WSTAMP(6);
     }
   }
+  WSTAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------

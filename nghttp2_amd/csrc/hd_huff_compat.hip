@@ -55,7 +55,7 @@ bool reserve(Single &s, size_t in_bytes, size_t out_bytes) {
     if (!hip_ok(hipMalloc(&s.d_meta, 64))) return false;
     if (!hip_ok(hipMalloc(&s.d_fs, 16)) || !hip_ok(hipMalloc(&s.d_fl, 16))) return false;
     s.ws = nghttp2_amd_hd_huff_workspace_size(1);
-    if (!hip_ok(hipMalloc(&s.d_ws, s.ws))) return false;
+    if (!hip_ok(hipMalloc(&s.d_ws, s.ws)) || !hip_ok(hipMemset(s.d_ws, 0, s.ws))) return false;
     s.failed = false;
     s.ready = true;
   }

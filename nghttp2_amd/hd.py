@@ -112,7 +112,8 @@ class HuffmanBatchCodec:
         else:
             need = self.L.nghttp2_amd_hd_huff_encode_workspace_size(int(raw_bytes), n)
         if self._ws is None or self._ws.numel() < need:
-            self._ws = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
+            # zeroed once; the engine keeps it consistent across calls (epochs)
+            self._ws = self.torch.zeros(need, dtype=self.torch.uint8, device=self.device)
         return self._ws
 
     def encode_bound(self, raw_bytes, n):

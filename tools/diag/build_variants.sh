@@ -1,10 +1,14 @@
 #!/bin/bash
 # Build ablation variants of the engine library into tools/diag/ (built in
 # the container; the .so files travel to the GPU box with the snapshot).
+# Usage: build_variants.sh name:"-DFLAG=1 -DX=2" ...   (name "cur" = no flags)
 set -e
 HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../../nghttp2_amd/csrc/hd_huff.hip
 rm -f $HERE/lib_*.so
-build() { name=$1; shift; (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 "$@" -o $HERE/lib_$name.so $SRC); echo built $name; }
-build ov16 -DSUB_OV=16u
-build ov24 -DSUB_OV=24u
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}; [ "$name" = "$spec" ] && flags=""
+  (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 $flags -o $HERE/lib_$name.so $SRC) &
+done
+wait
+ls $HERE/lib_*.so

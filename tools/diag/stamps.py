@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-phase cycle shares of k_decode from the HD_DIAG_STAMPS build."""
+"""Per-phase cycle shares of k_decode from the HD_DIAG_STAMPS build
+(tools/diag/lib_stamps.so): one row of s_memtime sums per wave."""
 import ctypes, json, os, sys
 import numpy as np
 import torch
@@ -8,7 +9,6 @@ sys.path.insert(0, os.path.join(HERE, "..", ".."))
 from nghttp2_amd import workloads as W
 import nghttp2_amd
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-WPG = 8  # waves per decode workgroup (DEC_NT / 64)
 dev = torch.device("cuda:0")
 pool, off = W.gen_pseudo_headers(1 << 20) if cfg == 2 else W.gen_mixed_values(1 << 20)
 codec = nghttp2_amd.HuffmanBatchCodec(dev)
@@ -25,21 +25,19 @@ s = torch.cuda.current_stream()
 def run():
     L.nghttp2_amd_hd_huff_decode_batch_auto(vp(enc.data_ptr()), vp(eo.data_ptr()), n, vp(dst.data_ptr()), cap,
         vp(doff.data_ptr()), vp(st.data_ptr()), None, None, vp(s.cuda_stream))
-run(); torch.cuda.synchronize()
+for _ in range(3): run()
+torch.cuda.synchronize()
 L.nghttp2_amd_hd__diag_stamps(None, 1)
-run(); torch.cuda.synchronize()
+a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+a.record(s); run(); b.record(s); torch.cuda.synchronize()
 buf = np.zeros((4096, 16), dtype=np.uint64)
 L.nghttp2_amd_hd__diag_stamps(vp(buf.ctypes.data), 0)
-names = ["tile", "stage+sort", "pass1", "verify", "scan", "pass2", "copyout", "unused"]
-tot = buf[:, :8].sum(axis=0).astype(float)
-used = buf[:, 11] > 0
-print(json.dumps({"config": cfg, "wgs": int(used.sum()),
-                  "share": {k: round(float(v / tot.sum()), 4) for k, v in zip(names, tot)},
-                  "cycles_per_wg_median": {k: float(np.median(buf[used, i])) for i, k in enumerate(names)},
-                  "verify_iters_per_round": float(buf[:, 8].sum() / max(1, buf[:, 10].sum())),
-                  "mismatches_per_round": float(buf[:, 9].sum() / max(1, buf[:, 10].sum())),
-                  "rounds": int(buf[:, 10].sum()), "tiles": int(buf[:, 11].sum()),
-                  "wave_trips_per_round": {"fast": float(buf[:, 12].sum() / max(1, buf[:, 10].sum()) / WPG),
-                                           "checked": float(buf[:, 13].sum() / max(1, buf[:, 10].sum()) / WPG),
-                                           "warm": float(buf[:, 14].sum() / max(1, buf[:, 10].sum()) / WPG)},
-                  "wave_pass1_cycles_per_round": float(buf[:, 15].sum() / max(1, buf[:, 10].sum()) / WPG)}, indent=1))
+names = ["setup", "stage", "pass1", "verify", "scan", "pass2", "roundend"]
+used = buf[:, 7] > 0
+B = buf[used].astype(float)
+life = B[:, 7]
+print(json.dumps({"config": cfg, "kernel_us": round(a.elapsed_time(b) * 1000, 1), "waves": int(used.sum()),
+                  "lifetime_cycles_median": float(np.median(life)), "lifetime_cycles_max": float(life.max()),
+                  "share_of_lifetime": {k: round(float(B[:, i].sum() / life.sum()), 4) for i, k in enumerate(names)},
+                  "cycles_per_round": {k: round(float(B[:, i].sum() / B[:, 9].sum()), 1) for i, k in enumerate(names)},
+                  "tasks_per_wave": float(B[:, 8].mean()), "rounds_per_wave": float(B[:, 9].mean())}, indent=1))

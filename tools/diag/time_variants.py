@@ -39,10 +39,11 @@ ecap = codec.encode_bound(int(off[-1]), n)
 edst = torch.empty(ecap, dtype=torch.uint8, device=dev)
 eoff = torch.empty(n + 1, dtype=torch.int32, device=dev)
 wsz = codec.L.nghttp2_amd_hd_huff_encode_workspace_size(int(off[-1]), n)
-ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+wss = {}
 def run_enc(L):
     L.nghttp2_amd_hd_huff_encode_batch(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(so.data_ptr()), n,
-        ctypes.c_void_p(edst.data_ptr()), ecap, ctypes.c_void_p(eoff.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+        ctypes.c_void_p(edst.data_ptr()), ecap, ctypes.c_void_p(eoff.data_ptr()),
+        ctypes.c_void_p(wss.setdefault(id(L), torch.zeros(wsz, dtype=torch.uint8, device=dev)).data_ptr()),
         wsz, ctypes.c_void_p(s.cuda_stream))
 eres = {k: [] for k in libs}
 ref_enc = enc[:E].clone()
