@@ -48,9 +48,6 @@ namespace host {
 
 // Ablation switch (tools/diag builds variants; the product uses the default)
 
-#ifndef HD_BITBUF
-#define HD_BITBUF 0  // fast loop: 1 = register bit buffer; 0 = LDS window per step (fewer VALU; faster at high occupancy)
-#endif
 #ifndef HD_DIAG_STAMPS
 #define HD_DIAG_STAMPS 0   // diagnostic build only: per-phase s_memtime sums
 #endif
@@ -633,9 +630,11 @@ enum { NLONG = 0 HD_HUFF_LONG_CODES(HD_COUNT_ROW) };  // code lengths > HD_HUFF_
 
 #define NLONG_PAD 16  // search width (padding rows repeat the last row)
 static_assert(NLONG <= NLONG_PAD, "long-code search too narrow");
-// Lookup entry (tools/gen_tables.py): sym1 | sym2 << 8 | L1 << 16 | cnt << 21 | used << 27
-#define E_L1(e) (((e) >> 16) & 31u)
-#define E_CNT(e) (((e) >> 21) & 3u)
+// Lookup entry (tools/gen_tables.py): sym1 | sym2 << 8 | 8 cnt << 16 | L1 << 21 | used << 27
+// (sym2 = 0 when cnt = 1: the low half is the entry's output bytes as they stand)
+#define E_CNT8(e) (((e) >> 16) & 0x18u)
+#define E_CNT(e) (((e) >> 19) & 3u)
+#define E_L1(e) (((e) >> 21) & 31u)
 #define E_USED(e) ((e) >> 27)
 struct DecTables {
   uint32_t lut[1 << HD_HUFF_LUT_BITS];
@@ -726,76 +725,79 @@ __device__ __forceinline__ uint32_t win_q(const lds_u32 *ibe, uint32_t q) {  // 
 }
 __device__ __forceinline__ uint32_t win_at(const lds_u32 *ibe, uint32_t bp) { return win_q(ibe, bp - 1u); }
 
-// Decode output sinks.  put2(v, cnt) appends cnt (1..2) symbols: sym1 in
-// bits 0..7 of v, sym2 in bits 8..15 (zero when cnt = 1).  Output goes straight
+// Decode output sinks.  put(v, c8) appends c8 / 8 (1..2) symbols: sym1 in
+// bits 0..7 of v, sym2 in bits 8..15 (zero when c8 = 8).  Output goes straight
 // to global memory: DwordSink for items that start an engine slot (dword
-// aligned), GlobalSink (bytes) for pieces that continue a string, whose
-// first byte shares a dword with the previous piece (another lane).
-struct GlobalSink {
-  uint8_t *p;
-  __device__ __forceinline__ uint32_t count() const { return (uint32_t)(uintptr_t)p; }
-  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
-    p[0] = (uint8_t)v;
-    if (cnt > 1) p[1] = (uint8_t)(v >> 8);
-    p += cnt;
-  }
-};
-// Direct global output of an item that starts on a dword boundary (an
-// engine slot): whole dwords from a 64-bit accumulator.  finish(): the
+// aligned), UDwordSink for pieces that continue a string (their first byte
+// may share a dword with the previous piece, another lane).
+//
+// Direct global output of an item that starts on a dword boundary: whole
+// dwords from a 64-bit accumulator holding nb pending bits.  finish(): the
 // string's last item may write its final dword whole (the slot is a dword
 // multiple and holds more than the decoded bytes); otherwise the tail goes
 // bytewise, since the next piece (another lane) continues in that dword.
 struct DwordSink {
-  uint32_t *p;
+  uint32_t *p, *p0;
   uint64_t acc;
-  uint32_t na, n;
+  uint32_t nb;
   __device__ __forceinline__ void init(uint8_t *q) {
-    p = reinterpret_cast<uint32_t *>(q);
+    p = p0 = reinterpret_cast<uint32_t *>(q);
     acc = 0;
-    na = n = 0;
+    nb = 0;
   }
-  __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
-    acc |= (uint64_t)v << (8u * na);
-    na += cnt;
-    n += cnt;
-    if (na >= 4u) {
+  __device__ __forceinline__ uint32_t count() const { return 4u * (uint32_t)(p - p0) + (nb >> 3); }
+  // put_nf: append without flushing (nb <= 31 before, so two of them fit)
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    acc |= (uint64_t)v << nb;
+    nb += c8;
+  }
+  __device__ __forceinline__ void flush() {
+    if (nb >= 32u) {
       *p++ = (uint32_t)acc;
       acc >>= 32;
-      na -= 4u;
+      nb -= 32u;
     }
   }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
+    put_nf(v, c8);
+    flush();
+  }
   __device__ __forceinline__ void finish(bool whole) {
-    if (na == 0) return;
+    if (nb == 0) return;
     if (whole) {
       *p = (uint32_t)acc;
     } else {
       uint8_t *b = reinterpret_cast<uint8_t *>(p);
-      for (uint32_t x = 0; x < na; ++x) b[x] = (uint8_t)(acc >> (8u * x));
+      for (uint32_t x = 0; x < (nb >> 3); ++x) b[x] = (uint8_t)(acc >> (8u * x));
     }
   }
 };
-// Direct global output of a piece that continues a string: its first byte
-// may share a dword with the previous piece (another lane), so that head
-// dword goes bytewise, every later complete dword whole, and the tail as
-// DwordSink::finish.
+// Direct global output of a piece that continues a string: the head dword
+// (shared with the previous piece) goes bytewise, every later complete dword
+// whole, and the tail as DwordSink::finish.
 struct UDwordSink {
   uint32_t *p;
   uint64_t acc;
-  uint32_t na, n, h;
+  uint32_t nb, n8, h;
   __device__ __forceinline__ void init(uint8_t *q) {
     h = (uint32_t)(uintptr_t)q & 3u;
     p = reinterpret_cast<uint32_t *>(q - h);
     acc = 0;
-    na = h;
-    n = 0;
+    nb = 8u * h;
+    n8 = 0;
   }
-  __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
-    acc |= (uint64_t)v << (8u * na);
-    na += cnt;
-    n += cnt;
-    if (na >= 4u) {
+  __device__ __forceinline__ uint32_t count() const { return n8 >> 3; }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    acc |= (uint64_t)v << nb;
+    nb += c8;
+    n8 += c8;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
+    put_nf(v, c8);
+    flush();
+  }
+  __device__ __forceinline__ void flush() {
+    if (nb >= 32u) {
       if (h) {  // the head dword: only bytes h..3 are this piece's
         uint8_t *b = reinterpret_cast<uint8_t *>(p);
         for (uint32_t x = h; x < 4u; ++x) b[x] = (uint8_t)(acc >> (8u * x));
@@ -805,10 +807,11 @@ struct UDwordSink {
       }
       ++p;
       acc >>= 32;
-      na -= 4u;
+      nb -= 32u;
     }
   }
   __device__ __forceinline__ void finish(bool whole) {
+    const uint32_t na = nb >> 3;
     if (na <= h) return;
     if (whole && h == 0) {
       *p = (uint32_t)acc;
@@ -819,9 +822,11 @@ struct UDwordSink {
   }
 };
 struct NullSink {
-  uint32_t n = 0;
-  __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t, uint32_t cnt) { n += cnt; }
+  uint32_t n8 = 0;
+  __device__ __forceinline__ uint32_t count() const { return n8 >> 3; }
+  __device__ __forceinline__ void put(uint32_t, uint32_t c8) { n8 += c8; }
+  __device__ __forceinline__ void put_nf(uint32_t, uint32_t c8) { n8 += c8; }
+  __device__ __forceinline__ void flush() {}
 };
 // Caller slots (any alignment, capacity checked).
 struct CheckedSink {
@@ -830,13 +835,15 @@ struct CheckedSink {
   bool ovf;
   __device__ __forceinline__ void init(uint8_t *q, uint32_t c) { p = q; cap = c; n = 0; ovf = false; }
   __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put2(uint32_t v, uint32_t cnt) {
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
     if (n < cap) p[n] = (uint8_t)v; else ovf = true;
-    if (cnt > 1) {
+    if (c8 > 8u) {
       if (n + 1 < cap) p[n + 1] = (uint8_t)(v >> 8); else ovf = true;
     }
-    n += cnt;
+    n += c8 >> 3;
   }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) { put(v, c8); }
+  __device__ __forceinline__ void flush() {}
 };
 
 // Code longer than the lookup: canonical length by a branch-free search over
@@ -852,7 +859,7 @@ __device__ __forceinline__ uint32_t long_entry(const DecTables &T, uint32_t win,
   const uint32_t L = T.long_len[i];
   const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
   if (L <= rem && sym == 256) return 0xFFFFFFFFu;
-  return (L <= rem ? sym : 0u) | (L << 16) | (1u << 21) | (L << 27);
+  return (L <= rem ? sym : 0u) | (8u << 16) | (L << 21) | (L << 27);
 }
 
 // First-level miss: the 13..16-bit second level, else the search.
@@ -897,71 +904,41 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
   }
   r.entry = bp;
   const uint32_t c0 = sink.count();
-  // fast: 2-symbol steps while bp + 12 < bstop and bp + 30 <= bend.  One
-  // loop exit: EOS (the FSM's sticky failure state) drops the bound.
-#if HD_BITBUF
-  // bb: valid bits MSB-aligned, nb >= 32 of them at the top of every step;
-  // nxt: the next staged word, loaded a refill ahead.  The dependent chain
-  // of a step is the table read and a 64-bit shift.
-  int32_t F = min((int32_t)bstop - 12, (int32_t)bend - 29);
-  if ((int32_t)bp < F) {
-    uint32_t wi = bp >> 5;
-    uint64_t bb = (((uint64_t)ibe[wi] << 32) | ibe[wi + 1]) << (bp & 31u);
-    uint32_t nb = 64u - (bp & 31u);
-    wi += 2;
-    uint32_t nxt = ibe[wi];
-    do {
-      DCTR(0);
-      const uint32_t w = (uint32_t)(bb >> 32);
-      uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
-      if (e == 0u) {
-        e = slow_entry(T, w, 30u);
-        if (e == 0xFFFFFFFFu) {
-          F = INT32_MIN;
-          e = 0u;
-        }
-      }
-      sink.put2(e & 0xFFFFu, E_CNT(e));
-      const uint32_t used = E_USED(e);
-      bp += used;
-      bb <<= used;
-      nb -= used;
-      const bool need = nb < 32u;
-      bb |= need ? ((uint64_t)nxt << (32u - nb)) : 0ull;
-      nb += need ? 32u : 0u;
-      wi += need ? 1u : 0u;
-      nxt = ibe[wi];
-    } while ((int32_t)bp < F);
-  }
-#else
+  // fast: 2-symbol steps while bp + 12 < bstop and bp + 30 <= bend, in pairs
+  // (one bound check and one sink flush per pair) while a whole pair fits,
+  // then single steps.  One loop exit: EOS (the FSM's sticky failure state)
+  // drops the bounds; a step at the EOS position emits nothing and does not
+  // move, so the rest of its pair is idempotent.
   int32_t F = min((int32_t)bstop - 13, (int32_t)bend - 30);  // bound for q = bp - 1
+  int32_t F2 = F - 30;  // a first step consumes <= 30 bits
   uint32_t q = bp - 1u;
+#define DEC_FAST_STEP()                                          \
+  do {                                                           \
+    const uint32_t w = win_q(ibe, q);                            \
+    uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];            \
+    if (e == 0u) {                                               \
+      e = slow_entry(T, w, 30u);                                 \
+      if (e == 0xFFFFFFFFu) {                                    \
+        F = F2 = INT32_MIN;                                      \
+        e = 0u;                                                  \
+      }                                                          \
+    }                                                            \
+    sink.put_nf(e & 0xFFFFu, E_CNT8(e));                         \
+    q += E_USED(e);                                              \
+  } while (0)
+  while ((int32_t)q < F2) {
+    DCTR(0);
+    DEC_FAST_STEP();
+    DEC_FAST_STEP();
+    sink.flush();
+  }
   while ((int32_t)q < F) {
     DCTR(0);
-#if HD_ABL_NOWIN  // timing ablation only (wrong output): no window read
-    const uint32_t w = q * 0x9E3779B9u;
-#else
-    const uint32_t w = win_q(ibe, q);
-#endif
-#if HD_ABL_NOLUT  // timing ablation only (wrong output): no lookup read
-    uint32_t e = (8u << 27) | (2u << 21) | (w >> 16);
-#else
-    uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
-#endif
-    if (e == 0u) {
-      e = slow_entry(T, w, 30u);
-      if (e == 0xFFFFFFFFu) {
-        F = INT32_MIN;
-        e = 0u;
-      }
-    }
-#if !HD_ABL_NOSINK  // timing ablation only (wrong output): no output
-    sink.put2(e & 0xFFFFu, E_CNT(e));
-#endif
-    q += E_USED(e);
+    DEC_FAST_STEP();
+    sink.flush();
   }
+#undef DEC_FAST_STEP
   bp = q + 1u;
-#endif
   bool failed = F == INT32_MIN;
   // checked: to the first boundary >= bstop, or the string's tail
   while (!failed && bp < bstop) {
@@ -985,7 +962,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
       break;
     }
     const bool two = E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
-    sink.put2(two ? e & 0xFFFFu : e & 0xFFu, two ? 2u : 1u);
+    sink.put(two ? e & 0xFFFFu : e & 0xFFu, two ? 16u : 8u);
     bp += two ? U : L1;
   }
   if (!failed && bp == bend) r.at_end = true;
@@ -1038,8 +1015,8 @@ struct ItemPos {
 // AUTO: engine slots (written to dst_off); else caller slots,
 // capacity-checked.
 struct DecShared {
+  DecTables T;  // first: the lookup sits at LDS offset 0 (its base folds into ds_read's offset)
   uint32_t ibe[DEC_WAVES][IBUF_W / 4 + 4];  // per wave: 16 spare bytes, then the round's input
-  DecTables T;
 };
 
 template <bool AUTO>
