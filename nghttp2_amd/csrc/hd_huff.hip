@@ -752,11 +752,21 @@ struct DwordSink {
     nb += c8;
   }
   __device__ __forceinline__ void flush() {
+#if HD_FLUSH_NOBRANCH
+    // the pending low dword goes out every time (a partial one is rewritten
+    // later, by this sink or by the next piece's head bytes)
+    *p = (uint32_t)acc;
+    const bool f = nb >= 32u;
+    p += f ? 1 : 0;
+    acc = f ? acc >> 32 : acc;
+    nb -= f ? 32u : 0u;
+#else
     if (nb >= 32u) {
       *p++ = (uint32_t)acc;
       acc >>= 32;
       nb -= 32u;
     }
+#endif
   }
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
     put_nf(v, c8);
