@@ -180,19 +180,26 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = B_total * args.steps / elapsed / 1e9
 
-    # roofline of the dominant kernel (k_decode: one launch per step)
+    # roofline of the dominant kernel: k_decode (one launch per step; the
+    # encode is three launches, k_enc_count + k_scan_tiles + k_encode, whose
+    # sum is reported beside it).  traffic: PMC-measured HBM bytes per launch
+    # of the same kernel on the same config (profiles/, FETCH_SIZE x 2 +
+    # WRITE_SIZE per MI355X_MICROARCH.md), when recorded.
     dec_alg = raw_bytes + enc_total + 12 * n  # reads E + offsets, writes R + status
     enc_alg = raw_bytes + enc_total + 12 * n
-    if t_dec >= t_enc:
-        kern, alg, tk = "k_decode", dec_alg, t_dec
-    else:
-        kern, alg, tk = "encode (k_enc_count+k_scan_tiles+k_encode)", enc_alg, t_enc
-    achieved = alg / tk / 1e9
-    roof = {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2),
+    achieved = dec_alg / t_dec / 1e9
+    traffic = None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath)).get("config%d" % args.config, {}).get("k_decode")
+        if tj and tj.get("strings") == n:
+            traffic = tj["hbm_bytes_per_launch"]
+    roof = {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None, "alg_bytes_per_launch": alg,
-            "launch_ms": round(tk * 1e3, 4), "enc_ms": round(t_enc * 1e3, 4),
-            "dec_ms": round(t_dec * 1e3, 4)}
+            "traffic": traffic, "alg_bytes_per_launch": dec_alg,
+            "launch_ms": round(t_dec * 1e3, 4), "dec_ms": round(t_dec * 1e3, 4),
+            "enc_ms": round(t_enc * 1e3, 4),
+            "enc_achieved": round(enc_alg / t_enc / 1e9, 2)}
 
     out = {"metric": "GB/s HPACK Huffman enc+dec (device-resident, batched headers)",
            "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
