@@ -118,6 +118,29 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, cons
                                      size_t workspace_size, void *stream);
 
 /*
+ * HPACK string literals, batched: emit_string (lib/nghttp2_hd.c:1001-1044)
+ * for N strings.  Literal i = dst[dst_off[i]..dst_off[i+1]) is
+ *   H | length    the H bit (0x80) iff the Huffman form is strictly shorter
+ *                 than the raw string (:1011), and the payload length as a
+ *                 7-bit-prefix integer (count_encoded_length / encode_length,
+ *                 :823-863, RFC 7541 5.1);
+ *   payload       the Huffman bytes (nghttp2_hd_huff_encode) or the raw ones.
+ * The literals are back to back in string order, ready to be spliced into
+ * header blocks in wire order.
+ *
+ *   raw_bytes : src_off[n] - src_off[0] (sizes the bounds below)
+ *   dst_cap   : >= nghttp2_amd_hd_emit_strings_bound(raw_bytes, n)
+ *   workspace : device scratch, 256-byte aligned,
+ *               >= nghttp2_amd_hd_emit_strings_workspace_size(raw_bytes, n)
+ */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_emit_strings_bound(uint64_t raw_bytes, uint32_t n);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_emit_strings_workspace_size(uint64_t raw_bytes, uint32_t n);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_off,
+                                      uint32_t n, uint64_t raw_bytes, uint8_t *dst,
+                                      size_t dst_cap, uint32_t *dst_off, void *workspace,
+                                      size_t workspace_size, void *stream);
+
+/*
  * Encoded lengths only: enc_len[i] = nghttp2_hd_huff_encode_count(string i)
  * (lib/nghttp2_hd_huffman.c:34-43).
  */

@@ -1296,6 +1296,114 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
+// HPACK string literals: emit_string (lib/nghttp2_hd.c:1001-1044), batched
+// ---------------------------------------------------------------------------
+// A literal is the H bit (0x80 iff the Huffman form is strictly shorter,
+// :1011) with the payload length as a 7-bit-prefix integer
+// (count_encoded_length / encode_length, :823-863), then the payload: the
+// Huffman bytes or the raw ones.  After a batch encode into the workspace,
+// k_frame_len sizes each literal, a tile scan places them, and k_frame_copy
+// writes the output stream dword by dword (coalesced stores), gathering each
+// byte from the prefix, the Huffman pool or the raw pool.
+
+// bytes of the 7-bit-prefix integer n (count_encoded_length(n, 7))
+__device__ __forceinline__ uint32_t prefix7_len(uint32_t n) {
+  if (n < 127u) return 1u;
+  n -= 127u;
+  uint32_t len = 2u;
+  for (; n >= 128u; n >>= 7) ++len;
+  return len;
+}
+// byte r of the literal's prefix (encode_length(buf, n, 7) with buf[0] = H)
+__device__ __forceinline__ uint32_t prefix7_byte(uint32_t n, uint32_t h, uint32_t r) {
+  if (r == 0) return (h << 7) | (n < 127u ? n : 127u);
+  const uint32_t m = (n - 127u) >> (7u * (r - 1u));
+  return (m & 0x7Fu) | (m >= 128u ? 0x80u : 0u);
+}
+
+// out_len[s] = literal bytes of string s; tile sums for the offset scan.
+__global__ __launch_bounds__(WG) void k_frame_len(const uint32_t *__restrict__ src_off,
+                                                  const uint32_t *__restrict__ enc_off, uint32_t n,
+                                                  uint32_t *__restrict__ out_len,
+                                                  uint32_t *__restrict__ tile_sums) {
+  __shared__ uint32_t red[WG / 64];
+  const uint32_t s = blockIdx.x * WG + threadIdx.x;
+  uint32_t f = 0;
+  if (s < n) {
+    const uint32_t R = src_off[s + 1] - src_off[s], E = enc_off[s + 1] - enc_off[s];
+    const uint32_t P = E < R ? E : R;
+    f = prefix7_len(P) + P;
+    out_len[s] = f;
+  }
+  uint32_t tot;
+  block_excl_scan<WG>(f, red, &tot);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+// One workgroup per tile of 256 literals: the tile's output bytes
+// [dst_off[t0], dst_off[t0 + 256]) go out as dwords, one per thread and
+// pass; a dword shared with a neighbouring tile goes bytewise.
+__global__ __launch_bounds__(WG) void k_frame_copy(const uint8_t *__restrict__ src,
+                                                   const uint32_t *__restrict__ src_off,
+                                                   const uint8_t *__restrict__ enc,
+                                                   const uint32_t *__restrict__ enc_off, uint32_t n,
+                                                   uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                                   const uint32_t *__restrict__ dst_off) {
+  __shared__ uint32_t fo[WG + 1];   // literal starts (tile-relative to nothing: absolute)
+  __shared__ uint32_t pay[WG];      // payload length | H << 31
+  __shared__ uint32_t psrc[WG];     // payload source offset (enc or src pool)
+  __shared__ uint8_t plen[WG];
+  const uint32_t t0 = blockIdx.x * WG;
+  const uint32_t nt = min(n - t0, (uint32_t)WG);
+  const uint32_t s = t0 + threadIdx.x;
+  if (threadIdx.x < nt) {
+    const uint32_t a = src_off[s], R = src_off[s + 1] - a;
+    const uint32_t e = enc_off[s], E = enc_off[s + 1] - e;
+    const bool h = E < R;
+    const uint32_t P = h ? E : R;
+    fo[threadIdx.x] = dst_off[s];
+    pay[threadIdx.x] = P | (h ? 0x80000000u : 0u);
+    psrc[threadIdx.x] = h ? e : a;
+    plen[threadIdx.x] = (uint8_t)prefix7_len(P);
+  }
+  if (threadIdx.x == 0) fo[nt] = dst_off[t0 + nt];
+  __syncthreads();
+  const uint32_t lo = fo[0], hi = fo[nt];
+  if (hi == lo) return;
+  for (uint32_t w = (lo >> 2) + threadIdx.x; w <= ((hi - 1u) >> 2); w += WG) {
+    const uint32_t p0 = 4u * w;
+    // the literal holding the first in-range byte of this dword
+    const uint32_t pf = max(p0, lo);
+    uint32_t a = 0, b = nt - 1u;
+    while (a < b) {  // last i with fo[i] <= pf
+      const uint32_t m = (a + b + 1u) >> 1;
+      if (fo[m] <= pf) a = m; else b = m - 1u;
+    }
+    uint32_t i = a, v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t p = p0 + j;
+      if (p < lo || p >= hi) continue;
+      while (p >= fo[i + 1]) ++i;  // empty literals do not exist: each has >= 1 byte
+      const uint32_t r = p - fo[i], L = plen[i], P = pay[i] & 0x7FFFFFFFu;
+      const bool h = pay[i] >> 31;
+      uint32_t byte;
+      if (r < L) byte = prefix7_byte(P, h ? 1u : 0u, r);
+      else byte = (h ? enc : src)[psrc[i] + (r - L)];
+      v |= byte << (8u * j);
+    }
+    if (p0 >= lo && p0 + 4u <= hi && p0 + 4u <= dst_cap) {
+      *reinterpret_cast<uint32_t *>(dst + p0) = v;
+    } else {
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t p = p0 + j;
+        if (p >= lo && p < hi && p < dst_cap) dst[p] = (uint8_t)(v >> (8u * j));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
@@ -1396,6 +1504,49 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
   hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+  return hip_rv(hipGetLastError());
+}
+
+size_t nghttp2_amd_hd_emit_strings_bound(uint64_t raw_bytes, uint32_t n) {
+  // a 32-bit length takes at most 6 prefix bytes (1 + ceil(32 / 7))
+  const uint64_t b = raw_bytes + 6u * (uint64_t)n + 16u;
+  return (size_t)((b + 15u) & ~(uint64_t)15u);
+}
+
+// workspace: [tile scratch][encoded offsets (n + 1)][encoded pool]
+static size_t a256(size_t x) { return (x + 255u) & ~(size_t)255u; }
+size_t nghttp2_amd_hd_emit_strings_workspace_size(uint64_t raw_bytes, uint32_t n) {
+  return a256(nghttp2_amd_hd_huff_workspace_size(n)) + a256(4u * ((size_t)n + 1u)) +
+         a256(nghttp2_amd_hd_huff_encode_bound(raw_bytes, n));
+}
+
+int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_off, uint32_t n,
+                                      uint64_t raw_bytes, uint8_t *dst, size_t dst_cap,
+                                      uint32_t *dst_off, void *workspace, size_t workspace_size,
+                                      void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !workspace) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)workspace & 255u) ||
+      workspace_size < nghttp2_amd_hd_emit_strings_workspace_size(raw_bytes, n) ||
+      dst_cap < nghttp2_amd_hd_emit_strings_bound(raw_bytes, n))
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  uint8_t *w = (uint8_t *)workspace;
+  uint32_t *tiles = (uint32_t *)w;
+  const size_t ws_t = a256(nghttp2_amd_hd_huff_workspace_size(n));
+  uint32_t *eoff = (uint32_t *)(w + ws_t);
+  uint8_t *epool = w + ws_t + a256(4u * ((size_t)n + 1u));
+  const size_t ecap = nghttp2_amd_hd_huff_encode_bound(raw_bytes, n);
+  int rv = nghttp2_amd_hd_huff_encode_batch(src, src_off, n, epool, ecap, eoff, tiles, ws_t, stream);
+  if (rv) return rv;
+  const uint32_t nt = ntiles_for(n);
+  hipLaunchKernelGGL(k_frame_len, dim3(nt), dim3(WG), 0, st, src_off, (const uint32_t *)eoff, n,
+                     dst_off, tiles);
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nt), dim3(WG), 0, st, dst_off, n, (const uint32_t *)tiles);
+  hipLaunchKernelGGL(k_frame_copy, dim3(nt), dim3(WG), 0, st, src, src_off, (const uint8_t *)epool,
+                     (const uint32_t *)eoff, n, dst, (uint64_t)dst_cap, (const uint32_t *)dst_off);
   return hip_rv(hipGetLastError());
 }
 

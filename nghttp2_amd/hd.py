@@ -65,6 +65,12 @@ def lib():
                                                             vp, vp]
         L.nghttp2_amd_hd_huff_decode_fsm_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp,
                                                            vp, vp, ctypes.c_int, vp]
+        u64 = ctypes.c_uint64
+        L.nghttp2_amd_hd_emit_strings_bound.restype = sz
+        L.nghttp2_amd_hd_emit_strings_bound.argtypes = [u64, u32]
+        L.nghttp2_amd_hd_emit_strings_workspace_size.restype = sz
+        L.nghttp2_amd_hd_emit_strings_workspace_size.argtypes = [u64, u32]
+        L.nghttp2_amd_hd_emit_strings_batch.argtypes = [vp, vp, u32, u64, vp, sz, vp, vp, sz, vp]
         _lib = L
     return _lib
 
@@ -105,6 +111,7 @@ class HuffmanBatchCodec:
         self.device = torch.device(device if device is not None else "cuda")
         self.L = lib()
         self._ws = None
+        self._ews = None
 
     def _workspace(self, n, raw_bytes=None):
         if raw_bytes is None:
@@ -145,6 +152,28 @@ class HuffmanBatchCodec:
             _p(src), _p(src_off), n, _p(enc_len), _stream(stream))
         _check(rv, "encode_count_batch")
         return enc_len[:n]
+
+    def emit_strings(self, src, src_off, raw_bytes=None, dst=None, dst_off=None, stream=None):
+        """HPACK string literals (emit_string, lib/nghttp2_hd.c:1001-1044) for
+        every string: returns (dst pool, dst_off int32[n+1]); literal i is
+        dst[dst_off[i]:dst_off[i+1]]."""
+        torch = self.torch
+        n = src_off.numel() - 1
+        if raw_bytes is None:
+            raw_bytes = src.numel()
+        cap = self.L.nghttp2_amd_hd_emit_strings_bound(int(raw_bytes), n)
+        if dst is None:
+            dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        if dst_off is None:
+            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+        need = self.L.nghttp2_amd_hd_emit_strings_workspace_size(int(raw_bytes), n)
+        if self._ews is None or self._ews.numel() < need:
+            self._ews = torch.empty(need, dtype=torch.uint8, device=self.device)
+        rv = self.L.nghttp2_amd_hd_emit_strings_batch(
+            _p(src), _p(src_off), n, int(raw_bytes), _p(dst), dst.numel(), _p(dst_off),
+            _p(self._ews), self._ews.numel(), _stream(stream))
+        _check(rv, "emit_strings_batch")
+        return dst, dst_off
 
     def decode_slots(self, src_off, dst_off=None, stream=None):
         n = src_off.numel() - 1

@@ -20,7 +20,9 @@
  *   - nghttp2_hd_huff_decode_context_init  lib/nghttp2_hd_huffman.c:106-109
  *   - nghttp2_hd_huff_decode         lib/nghttp2_hd_huffman.c:111-143
  *   - nghttp2_hd_huff_decode_failure_state lib/nghttp2_hd_huffman.c:145-147
- *   - emit_string's Huffman/raw choice  lib/nghttp2_hd.c:1009-1016
+ *   - emit_string (Huffman/raw choice, H bit, 7-bit-prefix length)
+ *     lib/nghttp2_hd.c:1001-1044, with count_encoded_length / encode_length
+ *     lib/nghttp2_hd.c:823-863
  *
  * Parity pinning: oracle/pin_reference.py runs the reference's own table
  * generator (mkhufftbl.py) in the build container and checks these tables
@@ -432,5 +434,75 @@ int orc_roundtrip_timed(const uint8_t *src, const uint32_t *src_off,
   double t2 = now_s();
   *t_enc = t1 - t0;
   *t_dec = t2 - t1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------
+ * HPACK string literal framing.
+ * ------------------------------------------------------------------ */
+
+/* count_encoded_length, lib/nghttp2_hd.c:823-838 */
+size_t orc_count_encoded_length(size_t n, size_t prefix) {
+  size_t k = ((size_t)1 << prefix) - 1;
+  size_t len = 0;
+  if (n < k) return 1;
+  n -= k;
+  ++len;
+  for (; n >= 128; n >>= 7, ++len)
+    ;
+  return len + 1;
+}
+
+/* encode_length, lib/nghttp2_hd.c:840-863: the prefix integer of RFC 7541
+ * 5.1 into buf, keeping the bits of buf[0] above the prefix. */
+size_t orc_encode_length(uint8_t *buf, size_t n, size_t prefix) {
+  size_t k = ((size_t)1 << prefix) - 1;
+  uint8_t *begin = buf;
+  *buf = (uint8_t)(*buf & ~k);
+  if (n < k) {
+    *buf = (uint8_t)(*buf | n);
+    return 1;
+  }
+  *buf = (uint8_t)(*buf | k);
+  ++buf;
+  n -= k;
+  for (; n >= 128; n >>= 7) *buf++ = (uint8_t)((1 << 7) | (n & 0x7F));
+  *buf++ = (uint8_t)n;
+  return (size_t)(buf - begin);
+}
+
+/* emit_string, lib/nghttp2_hd.c:1001-1044, into one flat buffer: the
+ * Huffman form iff nghttp2_hd_huff_encode_count(str) < len, the H bit
+ * (0x80) and the 7-bit-prefix length, then the payload.  Returns the bytes
+ * written (dst must hold orc_count_encoded_length(len, 7) + len). */
+size_t orc_emit_string(uint8_t *dst, const uint8_t *str, size_t len) {
+  size_t enclen = orc_encode_count(str, len);
+  int huffman = 0;
+  if (enclen < len) {
+    huffman = 1;
+  } else {
+    enclen = len;
+  }
+  const size_t blocklen = orc_count_encoded_length(enclen, 7);
+  dst[0] = huffman ? 1 << 7 : 0;
+  orc_encode_length(dst, enclen, 7);
+  if (huffman) {
+    size_t w = 0;
+    orc_encode(dst + blocklen, enclen, str, len, &w);
+  } else if (len) {
+    memcpy(dst + blocklen, str, len);
+  }
+  return blocklen + enclen;
+}
+
+/* Batch: dst_off[n+1] (OUT) and the literals back to back. */
+int orc_emit_strings_batch(const uint8_t *src, const uint32_t *src_off, uint32_t n,
+                           uint8_t *dst, uint32_t *dst_off) {
+  uint64_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    dst_off[i] = (uint32_t)o;
+    o += orc_emit_string(dst + o, src + src_off[i], src_off[i + 1] - src_off[i]);
+  }
+  dst_off[n] = (uint32_t)o;
   return 0;
 }

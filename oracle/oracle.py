@@ -57,6 +57,13 @@ def lib():
         L.orc_roundtrip_timed.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp,
                                           ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double)]
+        L.orc_count_encoded_length.restype = ctypes.c_size_t
+        L.orc_count_encoded_length.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
+        L.orc_encode_length.restype = ctypes.c_size_t
+        L.orc_encode_length.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t]
+        L.orc_emit_string.restype = ctypes.c_size_t
+        L.orc_emit_string.argtypes = [u8p, u8p, ctypes.c_size_t]
+        L.orc_emit_strings_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp]
         if L.orc_init() != 0:
             raise RuntimeError("oracle table construction failed")
         _lib = L
@@ -163,6 +170,36 @@ def decode_batch(enc, enc_off, dst_off=None, nthreads=1):
     lib().orc_decode_batch(_ptr(enc), _ptr(enc_off), n, _ptr(dst_off), _ptr(dst),
                            _ptr(status), _ptr(fstate), _ptr(flags), nthreads)
     return dst, dst_off, status, fstate, flags
+
+
+def encode_length(n, prefix, first=0):
+    """encode_length (lib/nghttp2_hd.c:840-863): the RFC 7541 5.1 prefix
+    integer, keeping the bits of `first` above the prefix."""
+    buf = (ctypes.c_uint8 * 16)(first)
+    k = lib().orc_encode_length(buf, n, prefix)
+    return bytes(buf[:k])
+
+
+def emit_string(data):
+    """emit_string (lib/nghttp2_hd.c:1001-1044): one HPACK string literal."""
+    p, n = _buf(data)
+    out = (ctypes.c_uint8 * (n + 16))()
+    k = lib().orc_emit_string(out, p, n)
+    return bytes(out[:k])
+
+
+def emit_strings_batch(pool, off):
+    """Batch of string literals back to back.  Returns (dst u8, dst_off u32[n+1])."""
+    pool = np.ascontiguousarray(pool, dtype=np.uint8)
+    if pool.size == 0:
+        pool = np.zeros(1, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    n = len(off) - 1
+    raw = int(off[-1]) - int(off[0]) if n else 0
+    dst = np.zeros(raw + 6 * n + 16, dtype=np.uint8)
+    dst_off = np.zeros(n + 1, dtype=np.uint32)
+    lib().orc_emit_strings_batch(_ptr(pool), _ptr(off), n, _ptr(dst), _ptr(dst_off))
+    return dst[:int(dst_off[-1])], dst_off
 
 
 def roundtrip_timed(pool, off, nthreads=1):

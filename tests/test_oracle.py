@@ -133,3 +133,33 @@ def test_golden_vectors_regression():
         assert np.array_equal(fl, g["flags"]), name
         assert hashlib.sha256(make_golden.decoded_bytes(dst, doff, st)).hexdigest() \
             == g["dec_sha256"], name
+
+
+# ---- HPACK string literal framing (emit_string) ----
+def test_oracle_prefix_integers_rfc7541():
+    ka = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    for v, prefix, hx, _cite in ka["rfc7541_integers"]["vectors"]:
+        assert O.encode_length(v, prefix).hex() == hx
+
+
+def test_oracle_string_literals_rfc7541():
+    ka = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    for s, hx, _cite in ka["rfc7541_string_literals"]["vectors"]:
+        assert O.emit_string(s.encode()).hex() == hx
+
+
+def test_oracle_emit_string_raw_and_long_lengths():
+    # Huffman only when strictly shorter (lib/nghttp2_hd.c:1011): raw for bytes
+    # whose codes are long, and multi-byte length prefixes from 127 on
+    for n in (0, 1, 126, 127, 128, 254, 255, 256, 16383 + 127, 16384 + 127, 70000):
+        raw = bytes(range(256)) * (n // 256 + 1)
+        raw = raw[:n]
+        out = O.emit_string(raw)
+        enclen = O.encode_count(raw)
+        huff = enclen < n
+        plen = len(O.encode_length(enclen if huff else n, 7))
+        assert out[0] >> 7 == (1 if huff else 0)
+        assert len(out) == plen + (enclen if huff else n)
+        if not huff:
+            assert out[plen:] == raw
+    assert O.emit_string(b"") == b"\x00"

@@ -304,3 +304,57 @@ def test_fsm_streaming_chunks(codec, dev):
     for i in range(n):
         if rst[i] >= 0:
             assert outs[0][i] + outs[1][i] == bytes(rd[rdo[i]:rdo[i] + rst[i]]), i
+
+
+# ---- HPACK string literals (emit_string) ----
+def gpu_emit(codec, dev, pool, off):
+    src = to_dev(pad16(pool, off[-1]), dev)
+    dst, dst_off = codec.emit_strings(src, to_dev(off, dev), raw_bytes=int(off[-1]))
+    do = dst_off.cpu().numpy().view(np.uint32).copy()
+    return dst.cpu().numpy()[:int(do[-1])], do
+
+
+def check_emit(codec, dev, pool, off, tag):
+    d, do = gpu_emit(codec, dev, pool, off)
+    rd, rdo = O.emit_strings_batch(pool, off)
+    assert np.array_equal(do, rdo), tag + ": literal offsets"
+    if not np.array_equal(d, rd):
+        i = int(np.nonzero(d != rd)[0][0])
+        s = int(np.searchsorted(do, i, side="right") - 1)
+        raise AssertionError("%s: literal byte %d differs (string %d)" % (tag, i, s))
+
+
+def test_emit_strings_rfc7541(codec, dev):
+    import json, os
+    ka = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+    vecs = ka["rfc7541_string_literals"]["vectors"]
+    strs = [v[0].encode() for v in vecs]
+    off = np.zeros(len(strs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(s) for s in strs])
+    pool = np.frombuffer(b"".join(strs), dtype=np.uint8)
+    d, do = gpu_emit(codec, dev, pool, off)
+    for i, v in enumerate(vecs):
+        assert bytes(d[do[i]:do[i + 1]]).hex() == v[1], v[2]
+
+
+@pytest.mark.parametrize("kind", ["pseudo", "mixed", "allbytes", "edge"])
+def test_emit_strings_parity(codec, dev, kind):
+    from nghttp2_amd import workloads as W
+    if kind == "pseudo":
+        pool, off = W.gen_pseudo_headers(20000)
+    elif kind == "mixed":
+        pool, off = W.gen_mixed_values(3000)
+    elif kind == "allbytes":
+        pool, off = W.gen_all_bytes(3000)
+    else:
+        # empty strings, raw-vs-Huffman choices and multi-byte length prefixes
+        rng = np.random.Generator(np.random.PCG64(0xE1))
+        strs = [b"", b"a", b"", bytes(range(256)), b"\xff" * 126, b"\xff" * 127,
+                b"\xff" * 128, b"a" * 126, b"a" * 127, b"a" * 160, b"a" * 254, b"a" * 255,
+                b"0" * (16383 + 127), b"0" * (16384 + 127), b"", b"\x00" * 300]
+        strs += [bytes(rng.integers(0, 256, size=int(k), dtype=np.uint8))
+                 for k in rng.integers(0, 400, size=500)]
+        off = np.zeros(len(strs) + 1, dtype=np.uint32)
+        off[1:] = np.cumsum([len(s) for s in strs])
+        pool = np.frombuffer(b"".join(strs), dtype=np.uint8)
+    check_emit(codec, dev, pool, off, kind)
