@@ -222,6 +222,68 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, 
                                          const uint8_t *init_flags, int final,
                                          void *stream);
 
+/* ------------------------------------------------------------------ */
+/* Batched HPACK inflate front-end               */
+/* ------------------------------------------------------------------ */
+/*
+ * An inflater is one connection's HPACK decoding context (dynamic table,
+ * table size settings), as nghttp2_hd_inflater (lib/nghttp2_hd.h).
+ * nghttp2_amd_hd_inflate_blocks decodes a batch of complete header blocks,
+ * block i against inflaters[i] (blocks of one connection in order), with
+ * every Huffman literal of the batch decoded in ONE GPU call.  Per block it
+ * behaves as nghttp2_hd_inflate_hd3 (nghttp2.h:6623) called with in_final=1
+ * until NGHTTP2_HD_INFLATE_FINAL, then nghttp2_hd_inflate_end_headers
+ * (nghttp2.h:6636): the same fields, the same dynamic table evolution, the
+ * same errors (NGHTTP2_ERR_HEADER_COMP, sticky per inflater).
+ */
+typedef struct nghttp2_amd_hd_inflater nghttp2_amd_hd_inflater;
+
+/* One emitted header field: name and value are NUL-terminated byte strings
+ * in the caller's arena; flags = NGHTTP2_NV_FLAG_NO_INDEX (1) for a
+ * never-indexed literal (nghttp2.h:574-613). */
+typedef struct {
+  uint32_t block;
+  uint32_t name_off, name_len;
+  uint32_t value_off, value_len;
+  uint8_t flags;
+} nghttp2_amd_hd_nv;
+
+/* nghttp2_hd_inflate_new (nghttp2.h:6277): dynamic table of 4096 bytes. */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_new(nghttp2_amd_hd_inflater **inflater_ptr);
+/* nghttp2_hd_inflate_del (nghttp2.h:6302) */
+NGHTTP2_AMD_EXTERN void nghttp2_amd_hd_inflate_del(nghttp2_amd_hd_inflater *inflater);
+/* nghttp2_hd_inflate_change_table_size (nghttp2.h:6331): a smaller value
+ * than the current maximum requires a size update at the head of the next
+ * block. */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_change_table_size(nghttp2_amd_hd_inflater *inflater,
+                                             size_t settings_max_dynamic_table_size);
+/* nghttp2_hd_inflate_get_num_table_entries / get_table_entry /
+ * get_dynamic_table_size / get_max_dynamic_table_size (nghttp2.h:6646-6678);
+ * idx is 1-based over static + dynamic table. */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_inflate_get_num_table_entries(nghttp2_amd_hd_inflater *inflater);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_get_table_entry(nghttp2_amd_hd_inflater *inflater,
+                                           size_t idx, const uint8_t **name, size_t *namelen,
+                                           const uint8_t **value, size_t *valuelen);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_inflate_get_dynamic_table_size(nghttp2_amd_hd_inflater *inflater);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_inflate_get_max_dynamic_table_size(nghttp2_amd_hd_inflater *inflater);
+
+/*
+ * Inflate nblocks complete header blocks (host memory).  Fields go to
+ * nva[0..*nva_used) in block order, their bytes to arena[0..*arena_used).
+ * block_status[i] = fields of block i, or NGHTTP2_AMD_ERR_HEADER_COMP (the
+ * fields before the error stay emitted, as the reference emits them one at
+ * a time; the inflater turns bad), or NGHTTP2_AMD_ERR_BUFFER_ERROR when
+ * nva / arena ran out (that block and the rest are not applied).  The GPU
+ * work is asynchronous on `stream` and synchronised before return; a batch
+ * without Huffman literals makes no GPU call.
+ */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters,
+                                  uint32_t nblocks, const uint8_t *const *blocks,
+                                  const size_t *block_lens, nghttp2_amd_hd_nv *nva,
+                                  size_t nva_cap, size_t *nva_used, uint8_t *arena,
+                                  size_t arena_cap, size_t *arena_used, int32_t *block_status,
+                                  void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,12 +8,14 @@ plumbing.  There is no CPU fallback: every compute call goes to the HIP
 library and raises if it is missing.
 """
 from .hd import (  # noqa: F401
+    HpackInflater,
     HuffmanBatchCodec,
     NGHTTP2_ERR_BUFFER_ERROR,
     NGHTTP2_ERR_HEADER_COMP,
     NGHTTP2_ERR_INVALID_ARGUMENT,
     lib,
     lib_path,
+    inflate_blocks,
     tables_ref_layout,
 )
 

@@ -45,6 +45,11 @@ def lib():
             raise RuntimeError(
                 "nghttp2_amd: HIP library %s is missing -- run "
                 "`python -c 'import __graft_entry__ as g; g.build()'`" % path)
+        # torch first: its HIP runtime (torch/lib/libamdhip64.so, soname
+        # libamdhip64.so.7) then also serves this library, so the process
+        # holds ONE runtime and torch's streams are valid here.  Loaded the
+        # other way round, torch brings a second runtime copy.
+        import torch  # noqa: F401
         L = ctypes.CDLL(path)
         vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
         L.nghttp2_amd_hd_version.restype = ctypes.c_char_p
@@ -260,3 +265,112 @@ class HuffmanBatchCodec:
         if want_ctx:
             return dst, dst_off, status[:n], fstate[:n], flags[:n]
         return dst, dst_off, status[:n]
+
+
+# ---------------------------------------------------------------------------
+# Batched HPACK inflate front-end (nghttp2_amd_hd_inflate_*)
+# ---------------------------------------------------------------------------
+class _Nv(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_uint32), ("name_off", ctypes.c_uint32),
+                ("name_len", ctypes.c_uint32), ("value_off", ctypes.c_uint32),
+                ("value_len", ctypes.c_uint32), ("flags", ctypes.c_uint8)]
+
+
+def _inflate_lib():
+    L = lib()
+    if not getattr(L, "_inflate_bound", False):
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.nghttp2_amd_hd_inflate_new.argtypes = [ctypes.POINTER(vp)]
+        L.nghttp2_amd_hd_inflate_del.argtypes = [vp]
+        L.nghttp2_amd_hd_inflate_del.restype = None
+        L.nghttp2_amd_hd_inflate_change_table_size.argtypes = [vp, sz]
+        L.nghttp2_amd_hd_inflate_get_num_table_entries.argtypes = [vp]
+        L.nghttp2_amd_hd_inflate_get_num_table_entries.restype = sz
+        L.nghttp2_amd_hd_inflate_get_table_entry.argtypes = [
+            vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.nghttp2_amd_hd_inflate_get_dynamic_table_size.argtypes = [vp]
+        L.nghttp2_amd_hd_inflate_get_dynamic_table_size.restype = sz
+        L.nghttp2_amd_hd_inflate_get_max_dynamic_table_size.argtypes = [vp]
+        L.nghttp2_amd_hd_inflate_get_max_dynamic_table_size.restype = sz
+        L.nghttp2_amd_hd_inflate_blocks.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, sz,
+                                                    ctypes.POINTER(sz), vp, sz,
+                                                    ctypes.POINTER(sz), vp, vp]
+        L._inflate_bound = True
+    return L
+
+
+class HpackInflater:
+    """One connection's HPACK decoding context (nghttp2_hd_inflater)."""
+
+    def __init__(self):
+        self.L = _inflate_lib()
+        p = ctypes.c_void_p()
+        _check(self.L.nghttp2_amd_hd_inflate_new(ctypes.byref(p)), "inflate_new")
+        self.p = p
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.nghttp2_amd_hd_inflate_del(self.p)
+            self.p = None
+
+    def change_table_size(self, settings_max):
+        _check(self.L.nghttp2_amd_hd_inflate_change_table_size(self.p, settings_max),
+               "inflate_change_table_size")
+
+    def dynamic_table(self):
+        """[(name, value)] of the dynamic table, most recent first."""
+        out = []
+        n = self.L.nghttp2_amd_hd_inflate_get_num_table_entries(self.p)
+        for idx in range(62, n + 1):
+            a, b = ctypes.c_void_p(), ctypes.c_void_p()
+            la, lb = ctypes.c_size_t(), ctypes.c_size_t()
+            _check(self.L.nghttp2_amd_hd_inflate_get_table_entry(
+                self.p, idx, ctypes.byref(a), ctypes.byref(la), ctypes.byref(b),
+                ctypes.byref(lb)), "inflate_get_table_entry")
+            out.append((ctypes.string_at(a, la.value) if la.value else b"",
+                        ctypes.string_at(b, lb.value) if lb.value else b""))
+        return out
+
+    def dynamic_table_size(self):
+        return self.L.nghttp2_amd_hd_inflate_get_dynamic_table_size(self.p)
+
+
+def inflate_blocks(inflaters, blocks, stream=None):
+    """Inflate complete header blocks, block i against inflaters[i], with
+    every Huffman literal decoded in one GPU batch.  Returns
+    (status[i], fields[i] = [(name, value, flags)])."""
+    L = _inflate_lib()
+    nb = len(blocks)
+    bufs = [bytes(b) for b in blocks]
+    keep = [ctypes.create_string_buffer(b, max(1, len(b))) for b in bufs]
+    ptrs = (ctypes.c_void_p * max(1, nb))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+    lens = (ctypes.c_size_t * max(1, nb))(*[len(b) for b in bufs])
+    infs = (ctypes.c_void_p * max(1, nb))(*[i.p.value for i in inflaters])
+    total = sum(len(b) for b in bufs)
+    nva_cap = total + 16
+    arena_cap = 8 * total + 64 * (total + 16) + 4096
+    nva = (_Nv * nva_cap)()
+    arena = (ctypes.c_uint8 * arena_cap)()
+    st = (ctypes.c_int32 * max(1, nb))()
+    nv_used, ar_used = ctypes.c_size_t(), ctypes.c_size_t()
+    s = None
+    if stream is not None:
+        s = ctypes.c_void_p(stream.cuda_stream)
+    else:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        except Exception:  # pragma: no cover - torch is part of the image
+            s = None
+    rv = L.nghttp2_amd_hd_inflate_blocks(infs, nb, ptrs, lens, nva, nva_cap,
+                                         ctypes.byref(nv_used), arena, arena_cap,
+                                         ctypes.byref(ar_used), st, s)
+    _check(rv, "inflate_blocks")
+    raw = bytes(arena[:ar_used.value])
+    fields = [[] for _ in range(nb)]
+    for k in range(nv_used.value):
+        r = nva[k]
+        fields[r.block].append((raw[r.name_off:r.name_off + r.name_len],
+                                raw[r.value_off:r.value_off + r.value_len], r.flags))
+    return [st[i] for i in range(nb)], fields

@@ -1,0 +1,188 @@
+"""oracle/hpack_oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+Pure-Python restatement of nghttp2's HPACK inflater, used as the parity
+checker of the batched inflate front-end (nghttp2_amd_hd_inflate_blocks).
+Nothing in the product imports it.  Huffman literals go through the C oracle
+(oracle/huff_oracle.c, nghttp2_hd_huff_decode with fin=1).
+
+Restates (citations are /root/reference paths):
+  nghttp2_hd_inflate_hd_nv          lib/nghttp2_hd.c:1919-2281 (in_final=1)
+  nghttp2_hd_inflate_end_headers    lib/nghttp2_hd.c:2283-2287
+  nghttp2_hd_inflate_change_table_size  lib/nghttp2_hd.c:1290-1322
+  decode_length                     lib/nghttp2_hd.c:882-945
+  hd_inflate_commit_indexed/newname/indname  lib/nghttp2_hd.c:1780-1875
+  add_hd_table_incremental          lib/nghttp2_hd.c:1130-1195
+  static table                      RFC 7541 Appendix A
+"""
+from . import oracle as O
+
+MAX_NV = 65536           # NGHTTP2_HD_MAX_NV
+ENTRY_OVERHEAD = 32      # NGHTTP2_HD_ENTRY_OVERHEAD
+DEFAULT_TABLE = 4096     # NGHTTP2_HD_DEFAULT_MAX_BUFFER_SIZE
+HEADER_COMP = -523
+NO_INDEX = 1             # NGHTTP2_NV_FLAG_NO_INDEX
+
+STATIC = [
+    (b":authority", b""), (b":method", b"GET"), (b":method", b"POST"), (b":path", b"/"),
+    (b":path", b"/index.html"), (b":scheme", b"http"), (b":scheme", b"https"),
+    (b":status", b"200"), (b":status", b"204"), (b":status", b"206"), (b":status", b"304"),
+    (b":status", b"400"), (b":status", b"404"), (b":status", b"500"),
+    (b"accept-charset", b""), (b"accept-encoding", b"gzip, deflate"),
+    (b"accept-language", b""), (b"accept-ranges", b""), (b"accept", b""),
+    (b"access-control-allow-origin", b""), (b"age", b""), (b"allow", b""),
+    (b"authorization", b""), (b"cache-control", b""), (b"content-disposition", b""),
+    (b"content-encoding", b""), (b"content-language", b""), (b"content-length", b""),
+    (b"content-location", b""), (b"content-range", b""), (b"content-type", b""),
+    (b"cookie", b""), (b"date", b""), (b"etag", b""), (b"expect", b""), (b"expires", b""),
+    (b"from", b""), (b"host", b""), (b"if-match", b""), (b"if-modified-since", b""),
+    (b"if-none-match", b""), (b"if-range", b""), (b"if-unmodified-since", b""),
+    (b"last-modified", b""), (b"link", b""), (b"location", b""), (b"max-forwards", b""),
+    (b"proxy-authenticate", b""), (b"proxy-authorization", b""), (b"range", b""),
+    (b"referer", b""), (b"refresh", b""), (b"retry-after", b""), (b"server", b""),
+    (b"set-cookie", b""), (b"strict-transport-security", b""), (b"transfer-encoding", b""),
+    (b"user-agent", b""), (b"vary", b""), (b"via", b""), (b"www-authenticate", b"")]
+assert len(STATIC) == 61
+
+
+class _Fail(Exception):
+    pass
+
+
+class Inflater:
+    def __init__(self):
+        self.table = []                  # [0] = most recent
+        self.size = 0
+        self.max = DEFAULT_TABLE         # ctx.hd_table_bufsize_max
+        self.settings_max = DEFAULT_TABLE
+        self.min_max = 0xFFFFFFFF
+        self.expect_size = False
+        self.bad = False
+
+    # lib/nghttp2_hd.c:1290-1322
+    def change_table_size(self, v):
+        self.settings_max = v
+        if self.max > v:
+            self.expect_size = True
+            self.min_max = v
+            self.max = v
+            self._shrink()
+
+    def _shrink(self):
+        while self.size > self.max and self.table:
+            n, v = self.table.pop()
+            self.size -= len(n) + len(v) + ENTRY_OVERHEAD
+
+    # add_hd_table_incremental, lib/nghttp2_hd.c:1130-1195
+    def _add(self, n, v):
+        room = len(n) + len(v) + ENTRY_OVERHEAD
+        while self.size + room > self.max and self.table:
+            a, b = self.table.pop()
+            self.size -= len(a) + len(b) + ENTRY_OVERHEAD
+        if room > self.max:
+            return
+        self.table.insert(0, (n, v))
+        self.size += room
+
+    def _get(self, idx):
+        return STATIC[idx] if idx < 61 else self.table[idx - 61]
+
+    def inflate_block(self, block):
+        """One complete block (in_final=1, then end_headers).  Returns
+        (status, fields): status = number of fields or HEADER_COMP; fields
+        emitted before an error are returned too (the reference emits them
+        one at a time)."""
+        fields = []
+        if self.bad:
+            return HEADER_COMP, fields
+        try:
+            self._inflate(bytes(block), fields)
+        except _Fail:
+            self.bad = True
+            return HEADER_COMP, fields
+        return len(fields), fields
+
+    def _inflate(self, b, fields):
+        pos = [0]
+        head = True
+
+        # decode_length, lib/nghttp2_hd.c:882-945 (with in_final)
+        def read_int(prefix, maxlen):
+            if pos[0] >= len(b):
+                raise _Fail()
+            k = (1 << prefix) - 1
+            n = b[pos[0]] & k
+            pos[0] += 1
+            if n == k:
+                shift = 0
+                while True:
+                    if pos[0] >= len(b):
+                        raise _Fail()
+                    c = b[pos[0]]
+                    pos[0] += 1
+                    add = c & 0x7F
+                    if shift >= 32 or (0xFFFFFFFF >> shift) < add:
+                        raise _Fail()
+                    add <<= shift
+                    if 0xFFFFFFFF - add < n:
+                        raise _Fail()
+                    n += add
+                    if not c & 0x80:
+                        break
+                    shift += 7
+            if n > maxlen:
+                raise _Fail()
+            return n
+
+        def read_str():
+            if pos[0] >= len(b):
+                raise _Fail()
+            huff = b[pos[0]] & 0x80
+            n = read_int(7, MAX_NV)
+            if len(b) - pos[0] < n:
+                raise _Fail()
+            s = b[pos[0]:pos[0] + n]
+            pos[0] += n
+            if huff:
+                rv, out, ctx = O.decode(s, final=1)
+                if rv < 0 or O.failure_state(ctx):
+                    raise _Fail()
+                return out
+            return s
+
+        while pos[0] < len(b):
+            c = b[pos[0]]
+            if self.expect_size and (c & 0xE0) != 0x20:
+                raise _Fail()
+            if (c & 0xE0) == 0x20:
+                if not head:
+                    raise _Fail()
+                v = read_int(5, min(self.min_max, self.settings_max))
+                self.min_max = 0xFFFFFFFF
+                self.expect_size = False
+                self.max = v
+                self._shrink()
+                continue
+            head = False
+            if c & 0x80:
+                idx = read_int(7, len(self.table) + 61)
+                if idx == 0:
+                    raise _Fail()
+                n, v = self._get(idx - 1)
+                fields.append((n, v, 0))
+                continue
+            index_required = bool(c & 0x40)
+            no_index = (c & 0xF0) == 0x10
+            if c in (0x40, 0x00, 0x10):
+                pos[0] += 1
+                name = read_str()
+            else:
+                idx = read_int(6 if index_required else 4, len(self.table) + 61)
+                if idx == 0:
+                    raise _Fail()
+                name = self._get(idx - 1)[0]
+            value = read_str()
+            if index_required:
+                self._add(name, value)
+            fields.append((name, value, NO_INDEX if no_index else 0))
+        if self.expect_size:  # the block ended in EXPECT_TABLE_SIZE (:2259-2266)
+            raise _Fail()
