@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--strings", type=int, default=None,
                     help="strings per GPU (configs 2/3) or in total (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="time replays of one HIP graph of the step instead of plain stream "
+                         "launches (slower on ROCm 7 here: 0.131 vs 0.124 ms per step)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-resident", action="store_true",
                     help="also time the pinned-host H2D+D2H round trip")
@@ -152,12 +155,31 @@ def main():
     idx = np.repeat(do[:-1], raw_len) + (np.arange(raw_bytes) - np.repeat(off[:-1].astype(np.int64), raw_len))
     assert np.array_equal(dh[idx], pool[:raw_bytes]), "decode(encode(x)) != x"
 
+    # per-kernel timing (roofline): K plain steps with events on the stream
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+
+    # the timed steps: plain launches on the stream (no events in between),
+    # or (--graph) replays of one HIP graph of the step's launches
+    graph = None
+    if args.graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(status.cpu().numpy(), raw_len), "graph replay mismatch"
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
