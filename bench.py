@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--strings", type=int, default=None,
                     help="strings per GPU (configs 2/3) or in total (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="pipeline the steps over this many streams (step i on stream i %% S)")
     ap.add_argument("--graph", action="store_true",
                     help="time replays of one HIP graph of the step instead of plain stream "
                          "launches (slower on ROCm 7 here: 0.131 vs 0.124 ms per step)")
@@ -116,34 +118,58 @@ def main():
         scaling = "strong"
     raw_bytes = int(off[-1])
 
-    codec = nghttp2_amd.HuffmanBatchCodec(dev)
     src = torch.from_numpy(pool).to(dev)
     src_off = torch.from_numpy(off.view(np.int32)).to(dev)
-    enc_cap = codec.encode_bound(raw_bytes, n)
-    enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
-    enc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    dec_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    dec_cap = codec.decode_bound(enc_cap, n)
-    dec = torch.empty(dec_cap, dtype=torch.uint8, device=dev)
-    status = torch.empty(n, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream()
+
+    class Pipe:
+        """One stream with its own output buffers and workspace: --streams S
+        pipelines S of them, step i on pipe i % S, so one step's decode can
+        overlap the next step's encode (independent batches; every step
+        does its whole encode + decode)."""
+
+        def __init__(self, stream):
+            self.codec = nghttp2_amd.HuffmanBatchCodec(dev)
+            self.stream = stream
+            self.enc_cap = self.codec.encode_bound(raw_bytes, n)
+            self.enc = torch.empty(self.enc_cap, dtype=torch.uint8, device=dev)
+            self.enc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            self.dec_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            self.dec = torch.empty(self.codec.decode_bound(self.enc_cap, n), dtype=torch.uint8,
+                                   device=dev)
+            self.status = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def run(self, evs=None):
+            st = self.stream
+            if evs is not None:
+                evs[0].record(st)
+            self.codec.encode(src, src_off, raw_bytes=raw_bytes, dst=self.enc,
+                              dst_off=self.enc_off, stream=st)
+            if evs is not None:
+                evs[1].record(st)
+            self.codec.decode_auto(self.enc, self.enc_off, dst=self.dec, dst_off=self.dec_off,
+                                   status=self.status, stream=st)
+            if evs is not None:
+                evs[2].record(st)
+
+    pipes = [Pipe(torch.cuda.current_stream() if k == 0 else torch.cuda.Stream(device=dev))
+             for k in range(max(1, args.streams))]
+    P0 = pipes[0]
+    codec, enc, enc_off, dec, dec_off, status = (P0.codec, P0.enc, P0.enc_off, P0.dec,
+                                                 P0.dec_off, P0.status)
+    stream = P0.stream
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
-        codec.encode(src, src_off, raw_bytes=raw_bytes, dst=enc, dst_off=enc_off)
-        if i is not None:
-            ev[i][1].record(stream)
-        codec.decode_auto(enc, enc_off, dst=dec, dst_off=dec_off, status=status)
-        if i is not None:
-            ev[i][2].record(stream)
+        P0.run(ev[i] if i is not None else None)
 
     for _ in range(args.warmup):
-        step()
+        for p in pipes:
+            p.run()
     torch.cuda.synchronize()
+    for p in pipes[1:]:  # every pipe decodes the batch exactly
+        assert torch.equal(p.status, P0.status) and torch.equal(p.enc_off, P0.enc_off)
 
     # correctness gate on this rank's batch (fails loudly, never measured)
     st = status.cpu().numpy()
@@ -179,7 +205,7 @@ def main():
         if graph is not None:
             graph.replay()
         else:
-            step()
+            pipes[i % len(pipes)].run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -234,7 +260,8 @@ def main():
                       "raw_bytes_per_gpu": raw_bytes, "enc_bytes_per_gpu": enc_total,
                       "E_over_R": round(enc_total / raw_bytes, 4),
                       "alg_bytes_per_step_all_gpus": int(B_total),
-                      "parallelism": "shard%d (independent batches, no collective)" % world},
+                      "parallelism": "shard%d (independent batches, no collective)" % world,
+                      "streams": len(pipes)},
            "roofline": roof}
 
     if args.host_resident:
