@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Throughput of the SURVEY.md 8(f) rows built beside the hot path:
+
+  emit     nghttp2_amd_hd_emit_strings_batch: HPACK string literals
+           (emit_string, lib/nghttp2_hd.c:1001-1044) for the config-2 batch,
+           device-resident; GB/s of raw in + literals out.
+  inflate  nghttp2_amd_hd_inflate_blocks: header blocks of many connections
+           (host memory), Huffman literals decoded in one GPU batch per
+           call; wire MB/s and fields/s, with the split between host passes
+           and the GPU round trip.
+
+Prints one JSON object.  Not the bench.py contract (that is the hot path
+itself); the numbers go to DESIGN.md."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def bench_emit(steps=20):
+    import torch
+    import nghttp2_amd
+    from nghttp2_amd import workloads as W
+    from oracle import oracle as O
+    dev = torch.device("cuda:0")
+    pool, off = W.gen_pseudo_headers(1 << 20)
+    raw = int(off[-1])
+    codec = nghttp2_amd.HuffmanBatchCodec(dev)
+    src = torch.from_numpy(pool).to(dev)
+    so = torch.from_numpy(off.view(np.int32)).to(dev)
+    dst, do = codec.emit_strings(src, so, raw_bytes=raw)
+    torch.cuda.synchronize()
+    # parity on a sample of the batch
+    k = 20000
+    rd, rdo = O.emit_strings_batch(pool, off[:k + 1])
+    assert np.array_equal(do[:k + 1].cpu().numpy().view(np.uint32), rdo)
+    assert np.array_equal(dst[:int(rdo[-1])].cpu().numpy(), rd)
+    for _ in range(3):
+        codec.emit_strings(src, so, raw_bytes=raw, dst=dst, dst_off=do)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        codec.emit_strings(src, so, raw_bytes=raw, dst=dst, dst_off=do)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    F = int(do[-1].item())
+    return {"strings": len(off) - 1, "raw_bytes": raw, "literal_bytes": F,
+            "ms_per_batch": round(t * 1e3, 4), "GBps_raw_plus_out": round((raw + F) / t / 1e9, 1)}
+
+
+def make_blocks(nconn, per_conn, fields_per_block, seed=7):
+    """Header blocks as a deflater would send them: repeated names indexed,
+    values as literals with incremental indexing (Huffman when shorter)."""
+    from oracle import oracle as O
+    from nghttp2_amd import workloads as W
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pool, off = W.gen_mixed_values(nconn * per_conn * fields_per_block, seed=seed, hi=120)
+    names = [b"cookie", b"user-agent", b"x-request-id", b"accept", b"referer", b"x-trace"]
+    blocks, conns = [], []
+    v = 0
+    for r in range(per_conn):
+        for c in range(nconn):
+            out = bytearray(b"\x82\x87")  # :method GET, :scheme https
+            for _ in range(fields_per_block):
+                name = names[rng.integers(0, len(names))]
+                val = bytes(pool[off[v]:off[v + 1]])
+                v += 1
+                out.append(0x00)  # literal without indexing, new name
+                out += O.emit_string(name)
+                out += O.emit_string(val)
+            blocks.append(bytes(out))
+            conns.append(c)
+    return blocks, conns
+
+
+def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
+    import nghttp2_amd
+    from oracle import hpack_oracle as HO
+    blocks, conns = make_blocks(nconn, per_conn, fields)
+    wire = sum(len(b) for b in blocks)
+    # parity on the first connection's blocks against the restatement
+    best = None
+    for _ in range(reps):
+        infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+        t0 = time.perf_counter()
+        st, f = nghttp2_amd.inflate_blocks([infs[c] for c in conns], blocks)
+        t = time.perf_counter() - t0
+        best = t if best is None or t < best else best
+    ref = HO.Inflater()
+    for k, (c, b) in enumerate(zip(conns, blocks)):
+        if c == 0:
+            assert ref.inflate_block(b) == (st[k], f[k])
+    nf = sum(len(x) for x in f)
+    return {"blocks": len(blocks), "connections": nconn, "fields": nf, "wire_bytes": wire,
+            "s_per_call": round(best, 4), "wire_MBps": round(wire / best / 1e6, 1),
+            "fields_per_s": round(nf / best), "note": "one call: host parse, one GPU decode of every "
+            "Huffman literal (H2D/D2H included), host replay; Python ctypes marshalling included"}
+
+
+if __name__ == "__main__":
+    print(json.dumps({"emit": bench_emit(), "inflate": bench_inflate()}, indent=1))
