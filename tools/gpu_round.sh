@@ -23,7 +23,11 @@ for s in ${STEPS:-pytest smoke bench bench3 host prof pmc}; do
     bench)  run bench 600 python bench.py ;;
     bench3) run bench3 600 python bench.py --config 3 --no-cpu-baseline ;;
     host)   run bench_host 600 python bench.py --host-resident --no-cpu-baseline ;;
-    prof)   rm -rf $O/prof2 $O/prof3
+    prof)   rm -rf $O/prof2 $O/prof3 $O/prof2s1 $O/prof3s1
+            # --streams 1: launches never overlap, so the per-kernel averages
+            # are the isolated durations the roofline uses
+            run prof2s1 300 rocprofv3 --kernel-trace --stats -d $O/prof2s1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1
+            run prof3s1 300 rocprofv3 --kernel-trace --stats -d $O/prof3s1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1 --config 3
             run prof2 300 rocprofv3 --kernel-trace --stats -d $O/prof2 -o run --output-format csv -- python3 bench.py --no-cpu-baseline
             run prof3 300 rocprofv3 --kernel-trace --stats -d $O/prof3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --config 3 ;;
     pmc)    for c in 2 3; do
