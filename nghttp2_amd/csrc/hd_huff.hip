@@ -141,6 +141,33 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sm,
   return wpre + inc - v;
 }
 
+// Exclusive scan of v and sum of w across the workgroup in one exchange.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan_sum(uint32_t v, uint32_t w, uint32_t *sm,
+                                                        uint32_t *total_v, uint32_t *total_w) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(v);
+  const uint32_t ws = __builtin_amdgcn_readlane(wave_incl_scan(w), 63);
+  if (lane == 63) {
+    sm[wid] = inc;
+    sm[NT / 64 + wid] = ws;
+  }
+  __syncthreads();
+  uint32_t wpre = 0, tv = 0, tw = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) {
+    const uint32_t x = sm[k];
+    if (k < wid) wpre += x;
+    tv += x;
+    tw += sm[NT / 64 + k];
+  }
+  __syncthreads();
+  *total_v = tv;
+  *total_w = tw;
+  return wpre + inc - v;
+}
+
 // Byte-stream writer for decode output: packs bytes into aligned 32-bit
 // words; partial words at the two ends go out byte by byte, so neighbouring
 // strings never overwrite each other's bytes.
@@ -436,13 +463,13 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_prefix) {
+                                               const uint32_t *__restrict__ tile_sums) {
   __shared__ uint2 codeT[512];                   // [256..511] = {0, 0}: bytes outside the wave
   __shared__ uint32_t image[ENC_WAVES][ENC_RW];
   __shared__ uint32_t heads[ENC_WAVES][36];
   __shared__ uint32_t cand[ENC_WAVES][65];
   __shared__ uint32_t o_sh[WG + 1];
-  __shared__ uint32_t red[WG / 64];
+  __shared__ uint32_t red[2 * (WG / 64)];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
   codeT[256 + threadIdx.x] = make_uint2(0u, 0u);
@@ -461,9 +488,24 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
   const uint32_t c_end = (Z + 15u) >> 4;
   uint4 wn = make_uint4(0, 0, 0, 0);  // the next round's chunk (prefetched)
   if ((A >> 4) + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + (((A >> 4) + lane) << 4));
-  uint32_t tot;
-  const uint32_t o_me = tile_prefix[blockIdx.x] + block_excl_scan<WG>(E_me, red, &tot);  // (barrier)
+  // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
+  // strings, L2-resident), summed with independent loads in flight
+  uint32_t pre = 0;
+  {
+    uint32_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t t = threadIdx.x;
+    for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p8[k] += tile_sums[t + k * WG];
+    }
+    for (; t < blockIdx.x; t += WG) pre += tile_sums[t];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pre += p8[k];
+  }
+  uint32_t tot, ptot;
+  const uint32_t o_me = block_excl_scan_sum<WG>(E_me, pre, red, &tot, &ptot) + ptot;  // (barriers)
   if (s_me < n) dst_off[s_me] = o_me;
+  if (s_me == n - 1u) dst_off[n] = o_me + E_me;
   o_sh[threadIdx.x] = o_me;
   if (threadIdx.x == WG - 1) o_sh[WG] = o_me + E_me;
   __syncthreads();
@@ -1501,7 +1543,6 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
   uint32_t *tiles = (uint32_t *)workspace;
   hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles,
                      (uint16_t *)nullptr, 1);
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
   hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
