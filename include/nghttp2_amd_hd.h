@@ -284,6 +284,64 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *co
                                   size_t arena_cap, size_t *arena_used, int32_t *block_status,
                                   void *stream);
 
+/* ------------------------------------------------------------------ */
+/* Batched HPACK deflate front-end                                      */
+/* ------------------------------------------------------------------ */
+/*
+ * A deflater is one connection's HPACK encoding context (nghttp2_hd_deflater,
+ * lib/nghttp2_hd.h).  nghttp2_amd_hd_deflate_blocks encodes a batch of
+ * header lists, list i with deflaters[i] (lists of one connection in
+ * order); every string literal of the batch is framed by ONE GPU call
+ * (nghttp2_amd_hd_emit_strings_batch).  Block i's wire is byte-identical to
+ * nghttp2_hd_deflate_hd2 (nghttp2.h:6127) on the same deflater state:
+ * the same table size updates, table search, indexing decisions (never
+ * index authorization, cookies shorter than 20 bytes and NO_INDEX fields;
+ * no indexing for :path, age, content-length, etag, if-modified-since,
+ * if-none-match, location, set-cookie and entries over 3/4 of the table)
+ * and the same Huffman-or-raw literals.
+ */
+typedef struct nghttp2_amd_hd_deflater nghttp2_amd_hd_deflater;
+
+/* Same layout as nghttp2_nv (nghttp2.h:574-613); flags bit 0 =
+ * NGHTTP2_NV_FLAG_NO_INDEX. */
+typedef struct {
+  const uint8_t *name;
+  const uint8_t *value;
+  size_t namelen;
+  size_t valuelen;
+  uint8_t flags;
+} nghttp2_amd_nv;
+
+/* nghttp2_hd_deflate_new (nghttp2.h:6003) */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_new(nghttp2_amd_hd_deflater **deflater_ptr,
+                               size_t max_deflate_dynamic_table_size);
+/* nghttp2_hd_deflate_del (nghttp2.h:6031) */
+NGHTTP2_AMD_EXTERN void nghttp2_amd_hd_deflate_del(nghttp2_amd_hd_deflater *deflater);
+/* nghttp2_hd_deflate_change_table_size (nghttp2.h:6057) */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_change_table_size(nghttp2_amd_hd_deflater *deflater,
+                                             size_t settings_max_dynamic_table_size);
+/* nghttp2_hd_deflate_get_num_table_entries / get_table_entry /
+ * get_dynamic_table_size (nghttp2.h:6221-6253); idx is 1-based. */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_deflate_get_num_table_entries(nghttp2_amd_hd_deflater *deflater);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_get_table_entry(nghttp2_amd_hd_deflater *deflater,
+                                           size_t idx, const uint8_t **name, size_t *namelen,
+                                           const uint8_t **value, size_t *valuelen);
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_deflate_get_dynamic_table_size(nghttp2_amd_hd_deflater *deflater);
+
+/*
+ * Deflate nblocks header lists (host memory): list i is
+ * nva[block_nv_off[i]..block_nv_off[i+1]).  Block i's wire is
+ * out[out_off[i]..out_off[i+1]); block_status[i] = its length, or
+ * NGHTTP2_AMD_ERR_HEADER_COMP for a deflater already bad, or
+ * NGHTTP2_AMD_ERR_BUFFER_ERROR when out_cap ran out (the deflater turns bad,
+ * as nghttp2_hd_deflate_hd2's INSUFF_BUFSIZE does).  The GPU work is
+ * asynchronous on `stream` and synchronised before return.
+ */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters,
+                                  uint32_t nblocks, const nghttp2_amd_nv *nva,
+                                  const uint32_t *block_nv_off, uint8_t *out, size_t out_cap,
+                                  uint32_t *out_off, int32_t *block_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

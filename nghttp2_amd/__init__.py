@@ -8,6 +8,7 @@ plumbing.  There is no CPU fallback: every compute call goes to the HIP
 library and raises if it is missing.
 """
 from .hd import (  # noqa: F401
+    HpackDeflater,
     HpackInflater,
     HuffmanBatchCodec,
     NGHTTP2_ERR_BUFFER_ERROR,
@@ -15,6 +16,7 @@ from .hd import (  # noqa: F401
     NGHTTP2_ERR_INVALID_ARGUMENT,
     lib,
     lib_path,
+    deflate_blocks,
     inflate_blocks,
     tables_ref_layout,
 )

@@ -1,0 +1,422 @@
+// hd_deflate.cpp -- batched HPACK deflate front-end (the
+// deflate side of rows 1 and 3).
+//
+// Host C++ above the C ABI.  Deflates many header lists (blocks of one or
+// many connections) per call; every string literal of the batch is framed by
+// ONE GPU call (nghttp2_amd_hd_emit_strings_batch: Huffman-or-raw choice,
+// H bit, length prefix, payload) instead of one emit_string per literal:
+//   pass 1  per block in order, against its deflater's dynamic table: table
+//           size updates, the table search, the indexing decision and the
+//           insertion -- the representation bytes, and the literals to frame;
+//   GPU     H2D of the literal strings, emit_strings, D2H of the literals;
+//   pass 2  the wire of each block: representation bytes and framed literals
+//           in order.
+// Output equals nghttp2_hd_deflate_hd2 (nghttp2.h:6127) per block:
+// nghttp2_hd_deflate_hd_bufs (lib/nghttp2_hd.c:1469-1505), deflate_nv
+// (:1373-1467), search_hd_table / search_static_table / hd_map_find
+// (:1201-1249, :566-589), hd_deflate_decide_indexing (:1358-1371),
+// emit_indexed_block / emit_indname_block / emit_newname_block /
+// emit_table_size (:975-1128), add_hd_table_incremental (:1130-1195).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <deque>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/nghttp2_amd_hd.h"
+
+namespace {
+
+const uint32_t kEntryOverhead = 32;
+const uint32_t kStaticLen = 61;
+const char *const kStatic[kStaticLen][2] = {
+    {":authority", ""}, {":method", "GET"}, {":method", "POST"}, {":path", "/"},
+    {":path", "/index.html"}, {":scheme", "http"}, {":scheme", "https"}, {":status", "200"},
+    {":status", "204"}, {":status", "206"}, {":status", "304"}, {":status", "400"},
+    {":status", "404"}, {":status", "500"}, {"accept-charset", ""},
+    {"accept-encoding", "gzip, deflate"}, {"accept-language", ""}, {"accept-ranges", ""},
+    {"accept", ""}, {"access-control-allow-origin", ""}, {"age", ""}, {"allow", ""},
+    {"authorization", ""}, {"cache-control", ""}, {"content-disposition", ""},
+    {"content-encoding", ""}, {"content-language", ""}, {"content-length", ""},
+    {"content-location", ""}, {"content-range", ""}, {"content-type", ""}, {"cookie", ""},
+    {"date", ""}, {"etag", ""}, {"expect", ""}, {"expires", ""}, {"from", ""}, {"host", ""},
+    {"if-match", ""}, {"if-modified-since", ""}, {"if-none-match", ""}, {"if-range", ""},
+    {"if-unmodified-since", ""}, {"last-modified", ""}, {"link", ""}, {"location", ""},
+    {"max-forwards", ""}, {"proxy-authenticate", ""}, {"proxy-authorization", ""},
+    {"range", ""}, {"referer", ""}, {"refresh", ""}, {"retry-after", ""}, {"server", ""},
+    {"set-cookie", ""}, {"strict-transport-security", ""}, {"transfer-encoding", ""},
+    {"user-agent", ""}, {"vary", ""}, {"via", ""}, {"www-authenticate", ""}};
+
+enum Mode { WITH_INDEXING, WITHOUT_INDEXING, NEVER_INDEXING };  // nghttp2_hd.h
+
+// lookup_token (lib/nghttp2_hd.c:137) restricted to what the deflater uses:
+// the first static-table index of a static name, else -1 (other tokens only
+// stand for name equality in the table search).
+int32_t static_token(const uint8_t *name, size_t len) {
+  for (uint32_t i = 0; i < kStaticLen; ++i)
+    if (strlen(kStatic[i][0]) == len && memcmp(kStatic[i][0], name, len) == 0) return (int32_t)i;
+  return -1;
+}
+bool name_is(const uint8_t *name, size_t len, const char *s) {
+  return strlen(s) == len && memcmp(s, name, len) == 0;
+}
+
+struct Entry {
+  std::string name, value;
+};
+
+// RFC 7541 5.1 prefix integer (encode_length, lib/nghttp2_hd.c:840-863)
+void put_int(std::string &out, uint32_t n, uint32_t prefix, uint8_t first) {
+  const uint32_t k = (1u << prefix) - 1u;
+  if (n < k) {
+    out.push_back((char)(first | n));
+    return;
+  }
+  out.push_back((char)(first | k));
+  n -= k;
+  for (; n >= 128u; n >>= 7) out.push_back((char)(0x80u | (n & 0x7Fu)));
+  out.push_back((char)n);
+}
+
+}  // namespace
+
+struct nghttp2_amd_hd_deflater {
+  std::deque<Entry> table;  // front = most recent
+  size_t bufsize = 0;
+  size_t bufsize_max;                   // ctx.hd_table_bufsize_max
+  size_t deflate_max;                   // deflate_hd_table_bufsize_max
+  size_t min_max = UINT32_MAX;          // min_hd_table_bufsize_max
+  bool notify = false;                  // notify_table_size_change
+  bool bad = false;
+
+  void shrink() {
+    while (bufsize > bufsize_max && !table.empty()) {
+      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
+      table.pop_back();
+    }
+  }
+  void add(const uint8_t *n, size_t nl, const uint8_t *v, size_t vl) {
+    const size_t room = nl + vl + kEntryOverhead;
+    while (bufsize + room > bufsize_max && !table.empty()) {
+      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
+      table.pop_back();
+    }
+    if (room > bufsize_max) return;
+    table.push_front(Entry{std::string((const char *)n, nl), std::string((const char *)v, vl)});
+    bufsize += room;
+  }
+};
+
+namespace {
+
+struct Engine {
+  std::mutex mu;
+  uint8_t *h_in = nullptr, *h_out = nullptr;
+  uint32_t *h_off = nullptr;
+  size_t hin_cap = 0, hout_cap = 0, hoff_cap = 0;
+  uint8_t *d_in = nullptr, *d_out = nullptr, *d_ws = nullptr;
+  uint32_t *d_off = nullptr;
+  size_t din_cap = 0, dout_cap = 0, dws_cap = 0, doff_cap = 0;
+};
+Engine &engine() {
+  static Engine e;
+  return e;
+}
+bool hip_ok(hipError_t e, const char *what) {
+  if (e == hipSuccess) return true;
+  fprintf(stderr, "nghttp2_amd_hd (deflate): %s: %s\n", what, hipGetErrorString(e));
+  return false;
+}
+bool grow_host(void **p, size_t *cap, size_t need) {
+  if (need <= *cap) return true;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (!hip_ok(hipHostMalloc(p, need, hipHostMallocDefault), "hipHostMalloc")) return false;
+  *cap = need;
+  return true;
+}
+bool grow_dev(void **p, size_t *cap, size_t need) {
+  if (need <= *cap) return true;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (!hip_ok(hipMalloc(p, need), "hipMalloc")) return false;
+  *cap = need;
+  return true;
+}
+
+// One piece of a block's wire: representation bytes, then up to two
+// literals (indices into the batch's literal list, -1 = none).
+struct Piece {
+  std::string bytes;
+  int32_t lit[2] = {-1, -1};
+};
+
+}  // namespace
+
+extern "C" {
+
+int nghttp2_amd_hd_deflate_new(nghttp2_amd_hd_deflater **deflater_ptr,
+                               size_t max_deflate_dynamic_table_size) {
+  if (!deflater_ptr) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  nghttp2_amd_hd_deflater *d = new (std::nothrow) nghttp2_amd_hd_deflater();
+  if (!d) return NGHTTP2_AMD_ERR_NOMEM;
+  // nghttp2_hd_deflate_new2 (lib/nghttp2_hd.c:721-748): the table starts at
+  // min(4096, max_deflate) and a smaller maximum is announced by a size update
+  d->deflate_max = max_deflate_dynamic_table_size;
+  d->bufsize_max = 4096;
+  if (max_deflate_dynamic_table_size < 4096) {
+    d->notify = true;
+    d->bufsize_max = max_deflate_dynamic_table_size;
+  }
+  *deflater_ptr = d;
+  return 0;
+}
+
+void nghttp2_amd_hd_deflate_del(nghttp2_amd_hd_deflater *deflater) { delete deflater; }
+
+int nghttp2_amd_hd_deflate_change_table_size(nghttp2_amd_hd_deflater *d,
+                                             size_t settings_max_dynamic_table_size) {
+  if (!d) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  const size_t next = settings_max_dynamic_table_size < d->deflate_max
+                          ? settings_max_dynamic_table_size : d->deflate_max;
+  d->bufsize_max = next;
+  d->min_max = d->min_max < next ? d->min_max : next;
+  d->notify = true;
+  d->shrink();
+  return 0;
+}
+
+size_t nghttp2_amd_hd_deflate_get_num_table_entries(nghttp2_amd_hd_deflater *d) {
+  return d ? d->table.size() + kStaticLen : 0;
+}
+
+int nghttp2_amd_hd_deflate_get_table_entry(nghttp2_amd_hd_deflater *d, size_t idx,
+                                           const uint8_t **name, size_t *namelen,
+                                           const uint8_t **value, size_t *valuelen) {
+  if (!d || idx == 0 || idx > d->table.size() + kStaticLen) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  --idx;
+  if (idx < kStaticLen) {
+    *name = (const uint8_t *)kStatic[idx][0];
+    *namelen = strlen(kStatic[idx][0]);
+    *value = (const uint8_t *)kStatic[idx][1];
+    *valuelen = strlen(kStatic[idx][1]);
+  } else {
+    const Entry &e = d->table[idx - kStaticLen];
+    *name = (const uint8_t *)e.name.data();
+    *namelen = e.name.size();
+    *value = (const uint8_t *)e.value.data();
+    *valuelen = e.value.size();
+  }
+  return 0;
+}
+
+size_t nghttp2_amd_hd_deflate_get_dynamic_table_size(nghttp2_amd_hd_deflater *d) {
+  return d ? d->bufsize : 0;
+}
+
+int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uint32_t nblocks,
+                                  const nghttp2_amd_nv *nva, const uint32_t *block_nv_off,
+                                  uint8_t *out, size_t out_cap, uint32_t *out_off,
+                                  int32_t *block_status, void *stream) {
+  if (nblocks == 0) {
+    if (out_off) out_off[0] = 0;
+    return 0;
+  }
+  if (!deflaters || !block_nv_off || !out_off || !block_status || (!nva && block_nv_off[nblocks]))
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  for (uint32_t i = 0; i < nblocks; ++i)
+    if (!deflaters[i] || block_nv_off[i] > block_nv_off[i + 1]) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+
+  // ---- pass 1: representations, in batch order
+  std::vector<std::vector<Piece>> pieces(nblocks);
+  std::vector<std::pair<const uint8_t *, uint32_t>> lits;
+  auto lit = [&](const uint8_t *p, size_t len) {
+    lits.emplace_back(p, (uint32_t)len);
+    return (int32_t)(lits.size() - 1);
+  };
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    nghttp2_amd_hd_deflater *d = deflaters[i];
+    std::vector<Piece> &P = pieces[i];
+    if (d->bad) {
+      block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
+      continue;
+    }
+    block_status[i] = 0;
+    if (d->notify) {  // nghttp2_hd_deflate_hd_bufs, lib/nghttp2_hd.c:1477-1494
+      const size_t mn = d->min_max;
+      d->notify = false;
+      d->min_max = UINT32_MAX;
+      Piece pc;
+      if (d->bufsize_max > mn) put_int(pc.bytes, (uint32_t)mn, 5, 0x20);
+      put_int(pc.bytes, (uint32_t)d->bufsize_max, 5, 0x20);
+      P.push_back(pc);
+    }
+    for (uint32_t k = block_nv_off[i]; k < block_nv_off[i + 1]; ++k) {
+      const nghttp2_amd_nv &nv = nva[k];
+      const int32_t token = static_token(nv.name, nv.namelen);
+      const size_t room = nv.namelen + nv.valuelen + kEntryOverhead;
+      // deflate_nv (:1373-1400): never-index authorization, short cookies
+      // and fields flagged NO_INDEX; hd_deflate_decide_indexing (:1358-1371)
+      Mode mode;
+      if (name_is(nv.name, nv.namelen, "authorization") ||
+          (name_is(nv.name, nv.namelen, "cookie") && nv.valuelen < 20) || (nv.flags & 1u)) {
+        mode = NEVER_INDEXING;
+      } else if (name_is(nv.name, nv.namelen, ":path") || name_is(nv.name, nv.namelen, "age") ||
+                 name_is(nv.name, nv.namelen, "content-length") ||
+                 name_is(nv.name, nv.namelen, "etag") ||
+                 name_is(nv.name, nv.namelen, "if-modified-since") ||
+                 name_is(nv.name, nv.namelen, "if-none-match") ||
+                 name_is(nv.name, nv.namelen, "location") ||
+                 name_is(nv.name, nv.namelen, "set-cookie") || room > d->bufsize_max * 3 / 4) {
+        mode = WITHOUT_INDEXING;
+      } else {
+        mode = WITH_INDEXING;
+      }
+      // search_hd_table (:1225-1249): the dynamic table newest first (an
+      // exact match, else the newest name match; name only when never
+      // indexing); a static name without a dynamic exact match searches the
+      // static table instead
+      const bool name_only = mode == NEVER_INDEXING;
+      int64_t idx = -1;
+      bool exact = false;
+      for (size_t t = 0; t < d->table.size(); ++t) {
+        const Entry &e = d->table[t];
+        if (e.name.size() != nv.namelen || memcmp(e.name.data(), nv.name, nv.namelen) != 0)
+          continue;
+        if (idx < 0) {
+          idx = (int64_t)(kStaticLen + t);
+          if (name_only) break;
+        }
+        if (e.value.size() == nv.valuelen && memcmp(e.value.data(), nv.value, nv.valuelen) == 0) {
+          idx = (int64_t)(kStaticLen + t);
+          exact = true;
+          break;
+        }
+      }
+      if (!exact && token >= 0) {  // search_static_table (:1201-1223)
+        idx = token;
+        if (!name_only) {
+          for (uint32_t s = (uint32_t)token; s < kStaticLen && name_is(nv.name, nv.namelen, kStatic[s][0]); ++s) {
+            if (strlen(kStatic[s][1]) == nv.valuelen && memcmp(kStatic[s][1], nv.value, nv.valuelen) == 0) {
+              idx = s;
+              exact = true;
+              break;
+            }
+          }
+        }
+      }
+      Piece pc;
+      if (exact) {  // emit_indexed_block (:975-993)
+        put_int(pc.bytes, (uint32_t)idx + 1u, 7, 0x80);
+        P.push_back(pc);
+        continue;
+      }
+      if (mode == WITH_INDEXING) d->add(nv.name, nv.namelen, nv.value, nv.valuelen);
+      const uint8_t first = mode == WITH_INDEXING ? 0x40 : mode == WITHOUT_INDEXING ? 0x00 : 0x10;
+      if (idx < 0) {  // emit_newname_block (:1104-1128)
+        pc.bytes.push_back((char)first);
+        pc.lit[0] = lit(nv.name, nv.namelen);
+      } else {  // emit_indname_block (:1062-1102)
+        put_int(pc.bytes, (uint32_t)idx + 1u, mode == WITH_INDEXING ? 6 : 4, first);
+      }
+      pc.lit[1] = lit(nv.value, nv.valuelen);
+      P.push_back(pc);
+    }
+  }
+
+  // ---- GPU: frame every literal of the batch (emit_string)
+  const uint32_t nl = (uint32_t)lits.size();
+  std::lock_guard<std::mutex> guard(engine().mu);
+  Engine &E = engine();
+  std::vector<uint32_t> loff(nl + 1, 0);
+  for (uint32_t k = 0; k < nl; ++k) loff[k + 1] = loff[k] + lits[k].second;
+  const uint8_t *fr = nullptr;
+  const uint32_t *froff = nullptr;
+  if (nl) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t raw = loff[nl];
+    const size_t in_bytes = ((size_t)raw + 15u) / 16u * 16u + 16u;
+    const size_t out_bytes = nghttp2_amd_hd_emit_strings_bound(raw, nl);
+    const size_t ws = nghttp2_amd_hd_emit_strings_workspace_size(raw, nl);
+    if (!grow_host((void **)&E.h_in, &E.hin_cap, in_bytes) ||
+        !grow_host((void **)&E.h_out, &E.hout_cap, out_bytes) ||
+        !grow_host((void **)&E.h_off, &E.hoff_cap, 2u * ((size_t)nl + 1u) * sizeof(uint32_t)) ||
+        !grow_dev((void **)&E.d_in, &E.din_cap, in_bytes) ||
+        !grow_dev((void **)&E.d_out, &E.dout_cap, out_bytes) ||
+        !grow_dev((void **)&E.d_ws, &E.dws_cap, ws) ||
+        !grow_dev((void **)&E.d_off, &E.doff_cap, 2u * ((size_t)nl + 1u) * sizeof(uint32_t)))
+      return NGHTTP2_AMD_ERR_NOMEM;
+    for (uint32_t k = 0; k < nl; ++k)
+      if (lits[k].second) memcpy(E.h_in + loff[k], lits[k].first, lits[k].second);
+    memset(E.h_in + raw, 0, in_bytes - raw);
+    memcpy(E.h_off, loff.data(), (nl + 1) * sizeof(uint32_t));
+    uint32_t *d_fo = E.d_off + (nl + 1);
+    uint32_t *h_fo = E.h_off + (nl + 1);
+    if (!hip_ok(hipMemcpyAsync(E.d_in, E.h_in, in_bytes, hipMemcpyHostToDevice, st), "H2D") ||
+        !hip_ok(hipMemcpyAsync(E.d_off, E.h_off, (nl + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st), "H2D"))
+      return NGHTTP2_AMD_ERR_FATAL;
+    int rv = nghttp2_amd_hd_emit_strings_batch(E.d_in, E.d_off, nl, raw, E.d_out, out_bytes, d_fo,
+                                               E.d_ws, ws, stream);
+    if (rv) return rv;
+    if (!hip_ok(hipMemcpyAsync(h_fo, d_fo, (nl + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "D2H") ||
+        !hip_ok(hipStreamSynchronize(st), "sync"))
+      return NGHTTP2_AMD_ERR_FATAL;
+    if (!hip_ok(hipMemcpyAsync(E.h_out, E.d_out, h_fo[nl], hipMemcpyDeviceToHost, st), "D2H") ||
+        !hip_ok(hipStreamSynchronize(st), "sync"))
+      return NGHTTP2_AMD_ERR_FATAL;
+    fr = E.h_out;
+    froff = h_fo;
+  }
+
+  // ---- pass 2: the wire of each block
+  size_t o = 0;
+  int ret = 0;
+  out_off[0] = 0;
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    const size_t o0 = o;
+    bool room = true;
+    if (block_status[i] == 0 && deflaters[i]->bad) {
+      // an earlier block of this deflater ran out of room in this call:
+      // later ones fail as nghttp2_hd_deflate_hd_bufs does (:1475-1477)
+      block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
+      out_off[i + 1] = (uint32_t)o;
+      continue;
+    }
+    for (const Piece &pc : pieces[i]) {
+      size_t need = pc.bytes.size();
+      for (int j = 0; j < 2; ++j)
+        if (pc.lit[j] >= 0) need += froff[pc.lit[j] + 1] - froff[pc.lit[j]];
+      if (o + need > out_cap) {
+        room = false;
+        break;
+      }
+      memcpy(out + o, pc.bytes.data(), pc.bytes.size());
+      o += pc.bytes.size();
+      for (int j = 0; j < 2; ++j) {
+        if (pc.lit[j] < 0) continue;
+        const uint32_t a = froff[pc.lit[j]], b = froff[pc.lit[j] + 1];
+        memcpy(out + o, fr + a, b - a);
+        o += b - a;
+      }
+    }
+    if (!room) {  // INSUFF_BUFSIZE in nghttp2_hd_deflate_hd2 (:1546-1547); the deflater turns bad
+      o = o0;
+      block_status[i] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+      deflaters[i]->bad = true;
+      ret = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+    } else if (block_status[i] == 0) {
+      block_status[i] = (int32_t)(o - o0);
+    }
+    out_off[i + 1] = (uint32_t)o;
+  }
+  return ret;
+}
+
+}  // extern "C"

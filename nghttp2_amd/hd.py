@@ -374,3 +374,107 @@ def inflate_blocks(inflaters, blocks, stream=None):
         fields[r.block].append((raw[r.name_off:r.name_off + r.name_len],
                                 raw[r.value_off:r.value_off + r.value_len], r.flags))
     return [st[i] for i in range(nb)], fields
+
+
+# ---------------------------------------------------------------------------
+# Batched HPACK deflate front-end (nghttp2_amd_hd_deflate_*)
+# ---------------------------------------------------------------------------
+class _NvIn(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_void_p), ("value", ctypes.c_void_p),
+                ("namelen", ctypes.c_size_t), ("valuelen", ctypes.c_size_t),
+                ("flags", ctypes.c_uint8)]
+
+
+def _deflate_lib():
+    L = _inflate_lib()
+    if not getattr(L, "_deflate_bound", False):
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.nghttp2_amd_hd_deflate_new.argtypes = [ctypes.POINTER(vp), sz]
+        L.nghttp2_amd_hd_deflate_del.argtypes = [vp]
+        L.nghttp2_amd_hd_deflate_del.restype = None
+        L.nghttp2_amd_hd_deflate_change_table_size.argtypes = [vp, sz]
+        L.nghttp2_amd_hd_deflate_get_num_table_entries.argtypes = [vp]
+        L.nghttp2_amd_hd_deflate_get_num_table_entries.restype = sz
+        L.nghttp2_amd_hd_deflate_get_table_entry.argtypes = [
+            vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.nghttp2_amd_hd_deflate_get_dynamic_table_size.argtypes = [vp]
+        L.nghttp2_amd_hd_deflate_get_dynamic_table_size.restype = sz
+        L.nghttp2_amd_hd_deflate_blocks.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, sz, vp, vp, vp]
+        L._deflate_bound = True
+    return L
+
+
+class HpackDeflater:
+    """One connection's HPACK encoding context (nghttp2_hd_deflater)."""
+
+    def __init__(self, max_deflate_table_size=4096):
+        self.L = _deflate_lib()
+        p = ctypes.c_void_p()
+        _check(self.L.nghttp2_amd_hd_deflate_new(ctypes.byref(p), max_deflate_table_size),
+               "deflate_new")
+        self.p = p
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.nghttp2_amd_hd_deflate_del(self.p)
+            self.p = None
+
+    def change_table_size(self, settings_max):
+        _check(self.L.nghttp2_amd_hd_deflate_change_table_size(self.p, settings_max),
+               "deflate_change_table_size")
+
+    def dynamic_table(self):
+        out = []
+        n = self.L.nghttp2_amd_hd_deflate_get_num_table_entries(self.p)
+        for idx in range(62, n + 1):
+            a, b = ctypes.c_void_p(), ctypes.c_void_p()
+            la, lb = ctypes.c_size_t(), ctypes.c_size_t()
+            _check(self.L.nghttp2_amd_hd_deflate_get_table_entry(
+                self.p, idx, ctypes.byref(a), ctypes.byref(la), ctypes.byref(b),
+                ctypes.byref(lb)), "deflate_get_table_entry")
+            out.append((ctypes.string_at(a, la.value) if la.value else b"",
+                        ctypes.string_at(b, lb.value) if lb.value else b""))
+        return out
+
+    def dynamic_table_size(self):
+        return self.L.nghttp2_amd_hd_deflate_get_dynamic_table_size(self.p)
+
+
+def deflate_blocks(deflaters, header_lists, stream=None):
+    """Encode header lists (each [(name, value[, flags])]), list i with
+    deflaters[i]; every literal framed in one GPU batch.  Returns
+    (status[i], wire[i])."""
+    L = _deflate_lib()
+    nb = len(header_lists)
+    flat = [(bytes(h[0]), bytes(h[1]), (h[2] if len(h) > 2 else 0))
+            for hl in header_lists for h in hl]
+    keep = []
+    nva = (_NvIn * max(1, len(flat)))()
+    for k, (n_, v_, fl) in enumerate(flat):
+        bn = ctypes.create_string_buffer(n_, max(1, len(n_)))
+        bv = ctypes.create_string_buffer(v_, max(1, len(v_)))
+        keep += [bn, bv]
+        nva[k].name = ctypes.cast(bn, ctypes.c_void_p)
+        nva[k].value = ctypes.cast(bv, ctypes.c_void_p)
+        nva[k].namelen, nva[k].valuelen, nva[k].flags = len(n_), len(v_), fl
+    offs = [0]
+    for hl in header_lists:
+        offs.append(offs[-1] + len(hl))
+    block_off = (ctypes.c_uint32 * (nb + 1))(*offs)
+    cap = sum(len(n_) + len(v_) + 16 for n_, v_, _ in flat) + 16 * nb + 64
+    out = (ctypes.c_uint8 * cap)()
+    out_off = (ctypes.c_uint32 * (nb + 1))()
+    st = (ctypes.c_int32 * max(1, nb))()
+    defl = (ctypes.c_void_p * max(1, nb))(*[d.p.value for d in deflaters])
+    s = None
+    if stream is not None:
+        s = ctypes.c_void_p(stream.cuda_stream)
+    else:
+        import torch
+        if torch.cuda.is_available():
+            s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rv = L.nghttp2_amd_hd_deflate_blocks(defl, nb, nva, block_off, out, cap, out_off, st, s)
+    if rv not in (0, NGHTTP2_ERR_BUFFER_ERROR):
+        _check(rv, "deflate_blocks")
+    raw = bytes(out[:out_off[nb]])
+    return [st[i] for i in range(nb)], [raw[out_off[i]:out_off[i + 1]] for i in range(nb)]

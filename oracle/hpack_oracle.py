@@ -186,3 +186,102 @@ class Inflater:
             fields.append((name, value, NO_INDEX if no_index else 0))
         if self.expect_size:  # the block ended in EXPECT_TABLE_SIZE (:2259-2266)
             raise _Fail()
+
+
+# ---------------------------------------------------------------------------
+# Deflater (nghttp2_hd_deflate_hd2 per block)
+# ---------------------------------------------------------------------------
+_NEVER, _WITHOUT, _WITH = 2, 1, 0
+_NO_INDEXING_NAMES = {b":path", b"age", b"content-length", b"etag", b"if-modified-since",
+                      b"if-none-match", b"location", b"set-cookie"}
+_STATIC_TOKEN = {}
+for _i, (_n, _v) in enumerate(STATIC):
+    _STATIC_TOKEN.setdefault(_n, _i)
+
+
+class Deflater:
+    """Restates nghttp2_hd_deflate_init2 (lib/nghttp2_hd.c:730-752),
+    nghttp2_hd_deflate_change_table_size (:1274-1288),
+    nghttp2_hd_deflate_hd_bufs (:1469-1505), deflate_nv (:1373-1467),
+    search_hd_table / search_static_table / hd_map_find (:1201-1249,
+    :566-589), hd_deflate_decide_indexing (:1358-1371) and the emit_*
+    helpers (:975-1128); string literals through the C oracle's emit_string."""
+
+    def __init__(self, max_deflate=4096):
+        self.table, self.size = [], 0
+        self.deflate_max = max_deflate
+        self.max = 4096
+        self.notify = False
+        self.min_max = 0xFFFFFFFF
+        if max_deflate < 4096:
+            self.notify, self.max = True, max_deflate
+
+    def change_table_size(self, v):
+        nxt = min(v, self.deflate_max)
+        self.max = nxt
+        self.min_max = min(self.min_max, nxt)
+        self.notify = True
+        while self.size > self.max and self.table:
+            a, b = self.table.pop()
+            self.size -= len(a) + len(b) + ENTRY_OVERHEAD
+
+    def _add(self, n, v):
+        room = len(n) + len(v) + ENTRY_OVERHEAD
+        while self.size + room > self.max and self.table:
+            a, b = self.table.pop()
+            self.size -= len(a) + len(b) + ENTRY_OVERHEAD
+        if room <= self.max:
+            self.table.insert(0, (n, v))
+            self.size += room
+
+    def deflate_block(self, fields):
+        out = bytearray()
+        if self.notify:
+            mn = self.min_max
+            self.notify, self.min_max = False, 0xFFFFFFFF
+            if self.max > mn:
+                out += O.encode_length(mn, 5, 0x20)
+            out += O.encode_length(self.max, 5, 0x20)
+        for f in fields:
+            n, v = bytes(f[0]), bytes(f[1])
+            flags = f[2] if len(f) > 2 else 0
+            token = _STATIC_TOKEN.get(n, -1)
+            if n == b"authorization" or (n == b"cookie" and len(v) < 20) or flags & NO_INDEX:
+                mode = _NEVER
+            elif n in _NO_INDEXING_NAMES or len(n) + len(v) + ENTRY_OVERHEAD > self.max * 3 // 4:
+                mode = _WITHOUT
+            else:
+                mode = _WITH
+            idx, exact = -1, False
+            for t, (a, b) in enumerate(self.table):
+                if a != n:
+                    continue
+                if idx < 0:
+                    idx = 61 + t
+                    if mode == _NEVER:
+                        break
+                if b == v:
+                    idx, exact = 61 + t, True
+                    break
+            if not exact and token >= 0:
+                idx = token
+                if mode != _NEVER:
+                    s = token
+                    while s < 61 and STATIC[s][0] == n:
+                        if STATIC[s][1] == v:
+                            idx, exact = s, True
+                            break
+                        s += 1
+            if exact:
+                out += O.encode_length(idx + 1, 7, 0x80)
+                continue
+            if mode == _WITH:
+                self._add(n, v)
+            first = (0x40, 0x00, 0x10)[mode]
+            if idx < 0:
+                out.append(first)
+                out += O.emit_string(n)
+            else:
+                out += O.encode_length(idx + 1, 6 if mode == _WITH else 4, first)
+            out += O.emit_string(v)
+        return bytes(out)
