@@ -327,6 +327,12 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_get_table_entry(nghttp2_amd_hd_def
                                            size_t idx, const uint8_t **name, size_t *namelen,
                                            const uint8_t **value, size_t *valuelen);
 NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_deflate_get_dynamic_table_size(nghttp2_amd_hd_deflater *deflater);
+/* nghttp2_hd_deflate_get_max_dynamic_table_size (nghttp2.h:6253) */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_deflate_get_max_dynamic_table_size(nghttp2_amd_hd_deflater *deflater);
+/* nghttp2_hd_deflate_bound (nghttp2.h:6209): an upper bound of one list's
+ * wire; the sum over a batch bounds out_cap. */
+NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_deflate_bound(nghttp2_amd_hd_deflater *deflater,
+                                    const nghttp2_amd_nv *nva, size_t nvlen);
 
 /*
  * Deflate nblocks header lists (host memory): list i is

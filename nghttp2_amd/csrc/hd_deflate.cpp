@@ -221,6 +221,20 @@ size_t nghttp2_amd_hd_deflate_get_dynamic_table_size(nghttp2_amd_hd_deflater *d)
   return d ? d->bufsize : 0;
 }
 
+size_t nghttp2_amd_hd_deflate_get_max_dynamic_table_size(nghttp2_amd_hd_deflater *d) {
+  return d ? d->bufsize_max : 0;
+}
+
+// nghttp2_hd_deflate_bound (lib/nghttp2_hd.c:1596-1621): two size updates of
+// at most 6 bytes, per field two 6-byte length prefixes plus the raw bytes.
+size_t nghttp2_amd_hd_deflate_bound(nghttp2_amd_hd_deflater *d, const nghttp2_amd_nv *nva,
+                                    size_t nvlen) {
+  (void)d;
+  size_t n = 12 + 12 * nvlen;
+  for (size_t i = 0; i < nvlen; ++i) n += nva[i].namelen + nva[i].valuelen;
+  return n;
+}
+
 int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uint32_t nblocks,
                                   const nghttp2_amd_nv *nva, const uint32_t *block_nv_off,
                                   uint8_t *out, size_t out_cap, uint32_t *out_off,

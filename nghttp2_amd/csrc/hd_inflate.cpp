@@ -71,21 +71,41 @@ struct nghttp2_amd_hd_inflater {
   bool expect_size = false;                     // NGHTTP2_HD_STATE_EXPECT_TABLE_SIZE
   bool bad = false;                             // ctx.bad
 
+  // Undo log of the block being applied: a block that runs out of caller
+  // buffer space is rolled back so the inflater is as before the call.
+  std::vector<Entry> evicted;  // in eviction order
+  size_t pushed = 0;
+
+  void evict() {
+    bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
+    evicted.push_back(std::move(table.back()));
+    table.pop_back();
+  }
   void shrink() {  // hd_context_shrink_table_size
-    while (bufsize > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+    while (bufsize > bufsize_max && !table.empty()) evict();
   }
   void add(const std::string &name, const std::string &value) {  // add_hd_table_incremental
     const size_t room = name.size() + value.size() + kEntryOverhead;
-    while (bufsize + room > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+    while (bufsize + room > bufsize_max && !table.empty()) evict();
     if (room > bufsize_max) return;
     table.push_front(Entry{name, value});
     bufsize += room;
+    ++pushed;
+  }
+  void begin_block() {
+    evicted.clear();
+    pushed = 0;
+  }
+  void rollback() {  // newest entries out, evicted ones back in reverse order
+    for (; pushed; --pushed) {
+      bufsize -= table.front().name.size() + table.front().value.size() + kEntryOverhead;
+      table.pop_front();
+    }
+    while (!evicted.empty()) {
+      bufsize += evicted.back().name.size() + evicted.back().value.size() + kEntryOverhead;
+      table.push_back(std::move(evicted.back()));
+      evicted.pop_back();
+    }
   }
   size_t max_index() const { return table.size() + kStaticLen; }  // get_max_index
 };
@@ -407,7 +427,10 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     const size_t nv0 = nv_n, ar0 = ar_n;
     bool ok = !inf->bad;
     bool head = true;  // size updates only at the head of a block
-    for (size_t k = 0; ok && k < bl[i].ops.size(); ++k) {
+    const size_t sv_max = inf->bufsize_max, sv_min = inf->min_max;
+    const bool sv_expect = inf->expect_size;
+    inf->begin_block();
+    for (size_t k = 0; ok && !full && k < bl[i].ops.size(); ++k) {
       const Op &op = bl[i].ops[k];
       if (inf->expect_size && op.kind != Op::SIZE) {
         ok = false;
@@ -460,6 +483,10 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     if (full) {
       nv_n = nv0;
       ar_n = ar0;
+      inf->rollback();
+      inf->bufsize_max = sv_max;
+      inf->min_max = sv_min;
+      inf->expect_size = sv_expect;
       for (uint32_t j = i; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
       break;
     }
