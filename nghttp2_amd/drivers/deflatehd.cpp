@@ -37,6 +37,7 @@ struct Config {
   bool http1text = false;            // -t
   bool dump_table = false;           // -d
   bool timing = false;               // --timing
+  int repeat = 0;                    // --repeat N: N more warm runs, best reported
   std::string out_dir;               // -o
 } cfg;
 
@@ -247,7 +248,8 @@ void usage() {
       "    -S, --deflate-table-size=<N>  use the first N bytes of the table (4096)\n"
       "    -d, --dump-header-table    output the dynamic table after each case\n"
       "    -o, --output-dir=<DIR>     write FILE's output to DIR/<basename FILE>\n"
-      "        --timing               batched call wall time to stderr (JSON)\n");
+      "        --timing               batched call wall time to stderr (JSON)\n"
+      "        --repeat=<N>           N more warm runs (fresh contexts); best in warm_seconds\n");
 }
 
 }  // namespace
@@ -259,6 +261,7 @@ int main(int argc, char **argv) {
                                            {"dump-header-table", no_argument, nullptr, 'd'},
                                            {"output-dir", required_argument, nullptr, 'o'},
                                            {"timing", no_argument, nullptr, 'T'},
+                                           {"repeat", required_argument, nullptr, 'R'},
                                            {"help", no_argument, nullptr, 'h'},
                                            {nullptr, 0, nullptr, 0}};
   for (;;) {
@@ -279,6 +282,7 @@ int main(int argc, char **argv) {
       case 'd': cfg.dump_table = true; break;
       case 'o': cfg.out_dir = optarg; break;
       case 'T': cfg.timing = true; break;
+      case 'R': cfg.repeat = atoi(optarg); break;
       default: return EXIT_FAILURE;
     }
   }
@@ -308,6 +312,7 @@ int main(int argc, char **argv) {
   std::vector<nghttp2_amd_hd_deflater *> defl;
   std::vector<nghttp2_amd_nv> nva;
   std::vector<uint32_t> nv_off{0};
+  std::vector<size_t> block_conn;
   size_t bound = 0, maxcases = 0;
   for (auto &c : conns) maxcases = std::max(maxcases, c.cases.size());
   for (size_t r = 0; r < maxcases; ++r)
@@ -316,6 +321,7 @@ int main(int argc, char **argv) {
       Case &k = c.cases[r];
       k.block = (uint32_t)defl.size();
       defl.push_back(c.d);
+      block_conn.push_back(&c - conns.data());
       nva.insert(nva.end(), k.nva.begin(), k.nva.end());
       nv_off.push_back((uint32_t)nva.size());
       bound += nghttp2_amd_hd_deflate_bound(c.d, k.nva.data(), k.nva.size());
@@ -348,6 +354,26 @@ int main(int argc, char **argv) {
     }
   }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  double warm = -1;
+  if (!cfg.dump_table && cfg.repeat > 0) {  // warm runs: fresh deflaters, same batch
+    std::vector<uint8_t> out2(out.size());
+    std::vector<uint32_t> off2(nb + 1);
+    std::vector<int32_t> st2(nb);
+    for (int r = 0; r < cfg.repeat; ++r) {
+      std::vector<nghttp2_amd_hd_deflater *> fresh(conns.size());
+      for (auto &f : fresh) f = init_deflater();
+      std::vector<nghttp2_amd_hd_deflater *> d2(nb);
+      for (uint32_t b = 0; b < nb; ++b) d2[b] = fresh[block_conn[b]];
+      const auto t1 = std::chrono::steady_clock::now();
+      const int rv = nghttp2_amd_hd_deflate_blocks(d2.data(), nb, nva.data(), nv_off.data(), out2.data(),
+                                                   out2.size(), off2.data(), st2.data(), nullptr);
+      const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+      if (rv < 0 || off2 != out_off || memcmp(out2.data(), out.data(), out_off[nb]) != 0)
+        die("warm run differs from the first run");
+      if (warm < 0 || t < warm) warm = t;
+      for (auto f : fresh) nghttp2_amd_hd_deflate_del(f);
+    }
+  }
 
   // ---- outputs, per connection in case order
   for (auto &c : conns) {
@@ -389,7 +415,7 @@ int main(int argc, char **argv) {
   if (cfg.timing)
     fprintf(stderr,
             "{\"timing\": {\"connections\": %zu, \"blocks\": %u, \"fields\": %zu, \"input_bytes\": %zu, "
-            "\"wire_bytes\": %zu, \"seconds\": %.6f, \"per_case_calls\": %s}}\n",
-            conns.size(), nb, nva.size(), input_sum, output_sum, secs, cfg.dump_table ? "true" : "false");
+            "\"wire_bytes\": %zu, \"seconds\": %.6f, \"warm_seconds\": %.6f, \"per_case_calls\": %s}}\n",
+            conns.size(), nb, nva.size(), input_sum, output_sum, secs, warm, cfg.dump_table ? "true" : "false");
   return 0;
 }
