@@ -23,12 +23,14 @@
 #include <string.h>
 
 #include <deque>
+#include <unordered_map>
 #include <mutex>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/nghttp2_amd_hd.h"
+#include "host_threads.h"
 
 namespace {
 
@@ -57,17 +59,38 @@ enum Mode { WITH_INDEXING, WITHOUT_INDEXING, NEVER_INDEXING };  // nghttp2_hd.h
 // lookup_token (lib/nghttp2_hd.c:137) restricted to what the deflater uses:
 // the first static-table index of a static name, else -1 (other tokens only
 // stand for name equality in the table search).
+size_t static_name_len(uint32_t i) {
+  static size_t lens[kStaticLen];
+  static bool init = [] {
+    for (uint32_t k = 0; k < kStaticLen; ++k) lens[k] = strlen(kStatic[k][0]);
+    return true;
+  }();
+  (void)init;
+  return lens[i];
+}
 int32_t static_token(const uint8_t *name, size_t len) {
   for (uint32_t i = 0; i < kStaticLen; ++i)
-    if (strlen(kStatic[i][0]) == len && memcmp(kStatic[i][0], name, len) == 0) return (int32_t)i;
+    if (static_name_len(i) == len && memcmp(kStatic[i][0], name, len) == 0) return (int32_t)i;
   return -1;
 }
 bool name_is(const uint8_t *name, size_t len, const char *s) {
   return strlen(s) == len && memcmp(s, name, len) == 0;
 }
 
+// FNV-1a of a name (the reference's name_hash, lib/nghttp2_hd.c:536-547):
+// the table search compares it before the bytes.
+uint32_t name_hash(const uint8_t *p, size_t n) {
+  uint32_t h = 2166136261u;
+  for (size_t i = 0; i < n; ++i) {
+    h ^= p[i];
+    h *= 16777619u;
+  }
+  return h;
+}
+
 struct Entry {
   std::string name, value;
+  uint32_t hash;
 };
 
 // RFC 7541 5.1 prefix integer (encode_length, lib/nghttp2_hd.c:840-863)
@@ -107,7 +130,7 @@ struct nghttp2_amd_hd_deflater {
       table.pop_back();
     }
     if (room > bufsize_max) return;
-    table.push_front(Entry{std::string((const char *)n, nl), std::string((const char *)v, vl)});
+    table.push_front(Entry{std::string((const char *)n, nl), std::string((const char *)v, vl), name_hash(n, nl)});
     bufsize += room;
   }
 };
@@ -248,19 +271,22 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   for (uint32_t i = 0; i < nblocks; ++i)
     if (!deflaters[i] || block_nv_off[i] > block_nv_off[i + 1]) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
 
-  // ---- pass 1: representations, in batch order
+  // ---- pass 1: representations; one task per connection, its lists in
+  // batch order (connections are independent)
+  using nghttp2_amd_host::parallel_for;
   std::vector<std::vector<Piece>> pieces(nblocks);
-  std::vector<std::pair<const uint8_t *, uint32_t>> lits;
-  auto lit = [&](const uint8_t *p, size_t len) {
-    lits.emplace_back(p, (uint32_t)len);
-    return (int32_t)(lits.size() - 1);
-  };
-  for (uint32_t i = 0; i < nblocks; ++i) {
-    nghttp2_amd_hd_deflater *d = deflaters[i];
+  std::vector<std::vector<std::pair<const uint8_t *, uint32_t>>> blits(nblocks);
+  auto deflate_list = [&](uint32_t i) {
+    std::vector<std::pair<const uint8_t *, uint32_t>> &L = blits[i];
+    auto lit = [&](const uint8_t *p, size_t len) {
+      L.emplace_back(p, (uint32_t)len);
+      return (int32_t)(L.size() - 1);
+    };
+      nghttp2_amd_hd_deflater *d = deflaters[i];
     std::vector<Piece> &P = pieces[i];
     if (d->bad) {
       block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
-      continue;
+      return;
     }
     block_status[i] = 0;
     if (d->notify) {  // nghttp2_hd_deflate_hd_bufs, lib/nghttp2_hd.c:1477-1494
@@ -275,6 +301,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     for (uint32_t k = block_nv_off[i]; k < block_nv_off[i + 1]; ++k) {
       const nghttp2_amd_nv &nv = nva[k];
       const int32_t token = static_token(nv.name, nv.namelen);
+      const uint32_t nh = name_hash(nv.name, nv.namelen);
       const size_t room = nv.namelen + nv.valuelen + kEntryOverhead;
       // deflate_nv (:1373-1400): never-index authorization, short cookies
       // and fields flagged NO_INDEX; hd_deflate_decide_indexing (:1358-1371)
@@ -302,7 +329,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
       bool exact = false;
       for (size_t t = 0; t < d->table.size(); ++t) {
         const Entry &e = d->table[t];
-        if (e.name.size() != nv.namelen || memcmp(e.name.data(), nv.name, nv.namelen) != 0)
+        if (e.hash != nh || e.name.size() != nv.namelen || memcmp(e.name.data(), nv.name, nv.namelen) != 0)
           continue;
         if (idx < 0) {
           idx = (int64_t)(kStaticLen + t);
@@ -343,19 +370,39 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
       pc.lit[1] = lit(nv.value, nv.valuelen);
       P.push_back(pc);
     }
+  };
+  {
+    std::unordered_map<nghttp2_amd_hd_deflater *, std::vector<uint32_t>> groups;
+    std::vector<nghttp2_amd_hd_deflater *> conns;
+    for (uint32_t i = 0; i < nblocks; ++i) {
+      auto &g = groups[deflaters[i]];
+      if (g.empty()) conns.push_back(deflaters[i]);
+      g.push_back(i);
+    }
+    parallel_for(conns.size(), 1, [&](size_t c) {
+      for (uint32_t i : groups[conns[c]]) deflate_list(i);
+    });
+  }
+  // literal numbering: block i's literals are litbase[i] + j
+  std::vector<uint32_t> litbase(nblocks + 1, 0);
+  std::vector<uint64_t> rawbase(nblocks + 1, 0);
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    uint64_t r = 0;
+    for (auto &l : blits[i]) r += l.second;
+    litbase[i + 1] = litbase[i] + (uint32_t)blits[i].size();
+    rawbase[i + 1] = rawbase[i] + r;
   }
 
   // ---- GPU: frame every literal of the batch (emit_string)
-  const uint32_t nl = (uint32_t)lits.size();
+  const uint32_t nl = litbase[nblocks];
   std::lock_guard<std::mutex> guard(engine().mu);
   Engine &E = engine();
-  std::vector<uint32_t> loff(nl + 1, 0);
-  for (uint32_t k = 0; k < nl; ++k) loff[k + 1] = loff[k] + lits[k].second;
   const uint8_t *fr = nullptr;
   const uint32_t *froff = nullptr;
   if (nl) {
     hipStream_t st = (hipStream_t)stream;
-    const uint64_t raw = loff[nl];
+    const uint64_t raw = rawbase[nblocks];
+    if (raw > UINT32_MAX) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
     const size_t in_bytes = ((size_t)raw + 15u) / 16u * 16u + 16u;
     const size_t out_bytes = nghttp2_amd_hd_emit_strings_bound(raw, nl);
     const size_t ws = nghttp2_amd_hd_emit_strings_workspace_size(raw, nl);
@@ -367,10 +414,18 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
         !grow_dev((void **)&E.d_ws, &E.dws_cap, ws) ||
         !grow_dev((void **)&E.d_off, &E.doff_cap, 2u * ((size_t)nl + 1u) * sizeof(uint32_t)))
       return NGHTTP2_AMD_ERR_NOMEM;
-    for (uint32_t k = 0; k < nl; ++k)
-      if (lits[k].second) memcpy(E.h_in + loff[k], lits[k].first, lits[k].second);
+    // the literal pool and its offsets, block by block
+    parallel_for(nblocks, 64, [&](size_t i) {
+      uint32_t o = (uint32_t)rawbase[i];
+      uint32_t k = litbase[i];
+      for (auto &l : blits[i]) {
+        E.h_off[k++] = o;
+        if (l.second) memcpy(E.h_in + o, l.first, l.second);
+        o += l.second;
+      }
+    });
+    E.h_off[nl] = (uint32_t)raw;
     memset(E.h_in + raw, 0, in_bytes - raw);
-    memcpy(E.h_off, loff.data(), (nl + 1) * sizeof(uint32_t));
     uint32_t *d_fo = E.d_off + (nl + 1);
     uint32_t *h_fo = E.h_off + (nl + 1);
     if (!hip_ok(hipMemcpyAsync(E.d_in, E.h_in, in_bytes, hipMemcpyHostToDevice, st), "H2D") ||
@@ -389,47 +444,55 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     froff = h_fo;
   }
 
-  // ---- pass 2: the wire of each block
+  // ---- pass 2: each block's wire size, placement in block order, then the
+  // bytes (representation bytes and framed literals, in order)
+  std::vector<size_t> need(nblocks, 0);
+  parallel_for(nblocks, 64, [&](size_t i) {
+    size_t n = 0;
+    for (const Piece &pc : pieces[i]) {
+      n += pc.bytes.size();
+      for (int j = 0; j < 2; ++j)
+        if (pc.lit[j] >= 0) {
+          const uint32_t g = litbase[i] + (uint32_t)pc.lit[j];
+          n += froff[g + 1] - froff[g];
+        }
+    }
+    need[i] = n;
+  });
   size_t o = 0;
   int ret = 0;
   out_off[0] = 0;
   for (uint32_t i = 0; i < nblocks; ++i) {
-    const size_t o0 = o;
-    bool room = true;
     if (block_status[i] == 0 && deflaters[i]->bad) {
       // an earlier block of this deflater ran out of room in this call:
       // later ones fail as nghttp2_hd_deflate_hd_bufs does (:1475-1477)
       block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
-      out_off[i + 1] = (uint32_t)o;
-      continue;
-    }
-    for (const Piece &pc : pieces[i]) {
-      size_t need = pc.bytes.size();
-      for (int j = 0; j < 2; ++j)
-        if (pc.lit[j] >= 0) need += froff[pc.lit[j] + 1] - froff[pc.lit[j]];
-      if (o + need > out_cap) {
-        room = false;
-        break;
-      }
-      memcpy(out + o, pc.bytes.data(), pc.bytes.size());
-      o += pc.bytes.size();
-      for (int j = 0; j < 2; ++j) {
-        if (pc.lit[j] < 0) continue;
-        const uint32_t a = froff[pc.lit[j]], b = froff[pc.lit[j] + 1];
-        memcpy(out + o, fr + a, b - a);
-        o += b - a;
-      }
-    }
-    if (!room) {  // INSUFF_BUFSIZE in nghttp2_hd_deflate_hd2 (:1546-1547); the deflater turns bad
-      o = o0;
+    } else if (block_status[i] == 0 && o + need[i] > out_cap) {
+      // INSUFF_BUFSIZE in nghttp2_hd_deflate_hd2 (:1546-1547); the deflater turns bad
       block_status[i] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
       deflaters[i]->bad = true;
       ret = NGHTTP2_AMD_ERR_BUFFER_ERROR;
     } else if (block_status[i] == 0) {
-      block_status[i] = (int32_t)(o - o0);
+      block_status[i] = (int32_t)need[i];
+      o += need[i];
     }
     out_off[i + 1] = (uint32_t)o;
   }
+  parallel_for(nblocks, 64, [&](size_t i) {
+    if (block_status[i] < 0) return;
+    uint8_t *w = out + out_off[i];
+    for (const Piece &pc : pieces[i]) {
+      memcpy(w, pc.bytes.data(), pc.bytes.size());
+      w += pc.bytes.size();
+      for (int j = 0; j < 2; ++j) {
+        if (pc.lit[j] < 0) continue;
+        const uint32_t g = litbase[i] + (uint32_t)pc.lit[j];
+        const uint32_t a = froff[g], b = froff[g + 1];
+        memcpy(w, fr + a, b - a);
+        w += b - a;
+      }
+    }
+  });
   return ret;
 }
 

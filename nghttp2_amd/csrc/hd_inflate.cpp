@@ -23,12 +23,14 @@
 #include <string.h>
 
 #include <deque>
+#include <unordered_map>
 #include <mutex>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/nghttp2_amd_hd.h"
+#include "host_threads.h"
 
 namespace {
 
@@ -71,41 +73,23 @@ struct nghttp2_amd_hd_inflater {
   bool expect_size = false;                     // NGHTTP2_HD_STATE_EXPECT_TABLE_SIZE
   bool bad = false;                             // ctx.bad
 
-  // Undo log of the block being applied: a block that runs out of caller
-  // buffer space is rolled back so the inflater is as before the call.
-  std::vector<Entry> evicted;  // in eviction order
-  size_t pushed = 0;
-
-  void evict() {
-    bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-    evicted.push_back(std::move(table.back()));
-    table.pop_back();
-  }
   void shrink() {  // hd_context_shrink_table_size
-    while (bufsize > bufsize_max && !table.empty()) evict();
+    while (bufsize > bufsize_max && !table.empty()) {
+      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
+      table.pop_back();
+    }
   }
-  void add(const std::string &name, const std::string &value) {  // add_hd_table_incremental
-    const size_t room = name.size() + value.size() + kEntryOverhead;
-    while (bufsize + room > bufsize_max && !table.empty()) evict();
+  // add_hd_table_incremental: e is built (copied) before any eviction, so a
+  // name taken from an entry that gets evicted stays valid
+  void add(Entry &&e) {
+    const size_t room = e.name.size() + e.value.size() + kEntryOverhead;
+    while (bufsize + room > bufsize_max && !table.empty()) {
+      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
+      table.pop_back();
+    }
     if (room > bufsize_max) return;
-    table.push_front(Entry{name, value});
+    table.push_front(std::move(e));
     bufsize += room;
-    ++pushed;
-  }
-  void begin_block() {
-    evicted.clear();
-    pushed = 0;
-  }
-  void rollback() {  // newest entries out, evicted ones back in reverse order
-    for (; pushed; --pushed) {
-      bufsize -= table.front().name.size() + table.front().value.size() + kEntryOverhead;
-      table.pop_front();
-    }
-    while (!evicted.empty()) {
-      bufsize += evicted.back().name.size() + evicted.back().value.size() + kEntryOverhead;
-      table.push_back(std::move(evicted.back()));
-      evicted.pop_back();
-    }
   }
   size_t max_index() const { return table.size() + kStaticLen; }  // get_max_index
 };
@@ -241,12 +225,151 @@ bool parse_block(const uint8_t *in, size_t len, Block &b) {
   return true;
 }
 
-// The Huffman literals of a block's parsed representations.
-void collect_huff(Block &b, std::vector<Lit *> &huff) {
-  for (Op &op : b.ops) {
-    if (op.kind != Op::LITERAL) continue;
-    if (op.name.huff == 0) huff.push_back(&op.name);
-    if (op.val.huff == 0) huff.push_back(&op.val);
+// Where pass 2 finds a literal's bytes: the wire, or the decoded pool.
+struct LitSrc {
+  const uint8_t *dec;
+  const uint32_t *slot;
+  const int32_t *st;
+  // false: -523 (bad padding or EOS, hd_inflate_read_huff :1740-1750)
+  bool get(const Lit &l, const char **p, size_t *n) const {
+    if (l.huff < 0) {
+      *p = (const char *)l.p;
+      *n = l.len;
+      return true;
+    }
+    const int32_t s = st[l.huff];
+    if (s < 0) return false;
+    *p = (const char *)dec + slot[l.huff];
+    *n = (size_t)s;
+    return true;
+  }
+};
+
+// One block's emitted fields: name\0value\0 runs in `bytes`.
+struct Rec {
+  uint32_t name_off, name_len, value_off, value_len;
+  uint8_t flags;
+};
+struct BlockOut {
+  std::vector<Rec> recs;
+  std::string bytes;
+  int32_t status = 0;
+};
+
+size_t static_len(uint32_t idx, int which) {
+  static size_t lens[kStaticLen][2];
+  static bool init = [] {
+    for (uint32_t i = 0; i < kStaticLen; ++i) {
+      lens[i][0] = strlen(kStatic[i][0]);
+      lens[i][1] = strlen(kStatic[i][1]);
+    }
+    return true;
+  }();
+  (void)init;
+  return lens[idx][which];
+}
+
+// Pass 2 for one block against its inflater (in order within a connection):
+// hd_inflate_commit_indexed / newname / indname (:1780-1875), the table size
+// update rules (:1942-2003), add_hd_table_incremental, and the end-of-block
+// checks; the bad state is sticky (:1932-1934, :2276).
+void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls, BlockOut &out) {
+  out.recs.clear();
+  out.bytes.clear();
+  auto emit = [&](const char *n, size_t nl, const char *v, size_t vl, uint8_t flags) {
+    Rec r;
+    r.flags = flags;
+    r.name_off = (uint32_t)out.bytes.size();
+    r.name_len = (uint32_t)nl;
+    out.bytes.append(n, nl);
+    out.bytes.push_back('\0');  // NUL-terminated like the reference's rcbufs (:2112, :2201)
+    r.value_off = (uint32_t)out.bytes.size();
+    r.value_len = (uint32_t)vl;
+    out.bytes.append(v, vl);
+    out.bytes.push_back('\0');
+    out.recs.push_back(r);
+  };
+  auto entry = [&](uint32_t idx, const char **n, size_t *nl, const char **v, size_t *vl) {
+    if (idx < kStaticLen) {
+      *n = kStatic[idx][0];
+      *nl = static_len(idx, 0);
+      *v = kStatic[idx][1];
+      *vl = static_len(idx, 1);
+    } else {
+      const Entry &e = inf->table[idx - kStaticLen];
+      *n = e.name.data();
+      *nl = e.name.size();
+      *v = e.value.data();
+      *vl = e.value.size();
+    }
+  };
+  bool ok = !inf->bad;
+  bool head = true;  // size updates only at the head of a block
+  for (size_t k = 0; ok && k < b.ops.size(); ++k) {
+    const Op &op = b.ops[k];
+    if (inf->expect_size && op.kind != Op::SIZE) {
+      ok = false;
+      break;
+    }
+    if (op.kind == Op::SIZE) {
+      if (!head || op.value > (inf->min_max < inf->settings_max ? inf->min_max : inf->settings_max)) {
+        ok = false;
+        break;
+      }
+      inf->expect_size = false;
+      inf->min_max = UINT32_MAX;
+      inf->bufsize_max = op.value;
+      inf->shrink();
+      continue;
+    }
+    head = false;
+    const char *n, *v;
+    size_t nl, vl;
+    if (op.kind == Op::INDEXED) {  // hd_inflate_commit_indexed
+      if (op.value == 0 || op.value > inf->max_index()) {
+        ok = false;
+        break;
+      }
+      entry(op.value - 1, &n, &nl, &v, &vl);
+      emit(n, nl, v, vl, 0);
+      continue;
+    }
+    if (op.new_name) {  // hd_inflate_commit_newname
+      if (!ls.get(op.name, &n, &nl)) {
+        ok = false;
+        break;
+      }
+    } else {  // hd_inflate_commit_indname
+      if (op.value == 0 || op.value > inf->max_index()) {
+        ok = false;
+        break;
+      }
+      const char *v0;
+      size_t vl0;
+      entry(op.value - 1, &n, &nl, &v0, &vl0);
+    }
+    if (!ls.get(op.val, &v, &vl)) {
+      ok = false;
+      break;
+    }
+    const uint8_t flags = op.no_index ? 1u : 0u;  // NGHTTP2_NV_FLAG_NO_INDEX
+    if (op.index_required) {
+      Entry e{std::string(n, nl), std::string(v, vl)};
+      emit(e.name.data(), e.name.size(), e.value.data(), e.value.size(), flags);
+      inf->add(std::move(e));
+    } else {
+      emit(n, nl, v, vl, flags);
+    }
+  }
+  // truncated or malformed wire after the parsed representations; and a
+  // block that ends while a table size update is still expected
+  // (lib/nghttp2_hd.c:2259-2266)
+  if (ok && (!b.parse_ok || inf->expect_size)) ok = false;
+  if (!ok) {
+    inf->bad = true;
+    out.status = NGHTTP2_AMD_ERR_HEADER_COMP;  // the fields before the error stay emitted
+  } else {
+    out.status = (int32_t)out.recs.size();
   }
 }
 
@@ -320,25 +443,42 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   for (uint32_t i = 0; i < nblocks; ++i)
     if (!inflaters[i] || (!blocks[i] && block_lens[i])) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
 
-  // ---- pass 1
+  // ---- pass 1: parse every block (stateless: one task per block)
+  using nghttp2_amd_host::parallel_for;
   std::vector<Block> bl(nblocks);
-  std::vector<Lit *> huff;
-  for (uint32_t i = 0; i < nblocks; ++i) {
+  std::vector<uint32_t> nhuff(nblocks + 1, 0);  // Huffman literals per block, then prefix
+  parallel_for(nblocks, 16, [&](size_t i) {
     // a malformed block keeps the representations before the error: the
     // reference emits those fields before it fails
     bl[i].parse_ok = parse_block(blocks[i], block_lens[i], bl[i]);
-    collect_huff(bl[i], huff);
+    uint32_t c = 0;
+    for (const Op &op : bl[i].ops)
+      if (op.kind == Op::LITERAL) c += (op.name.huff == 0) + (op.val.huff == 0);
+    nhuff[i + 1] = c;
+  });
+  for (uint32_t i = 0; i < nblocks; ++i) nhuff[i + 1] += nhuff[i];
+  const uint32_t nh = nhuff[nblocks];
+  std::vector<const Lit *> huff(nh);
+  std::vector<uint32_t> hoff(nh + 1, 0);
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    uint32_t k = nhuff[i];
+    for (Op &op : bl[i].ops) {
+      if (op.kind != Op::LITERAL) continue;
+      if (op.name.huff == 0) {
+        op.name.huff = (int32_t)k;
+        huff[k++] = &op.name;
+      }
+      if (op.val.huff == 0) {
+        op.val.huff = (int32_t)k;
+        huff[k++] = &op.val;
+      }
+    }
   }
+  for (uint32_t k = 0; k < nh; ++k) hoff[k + 1] = hoff[k] + huff[k]->len;
 
   // ---- GPU: every Huffman literal of the batch in one decode
   std::lock_guard<std::mutex> guard(engine().mu);
   Engine &E = engine();
-  const uint32_t nh = (uint32_t)huff.size();
-  std::vector<uint32_t> hoff(nh + 1, 0);
-  for (uint32_t k = 0; k < nh; ++k) {
-    huff[k]->huff = (int32_t)k;
-    hoff[k + 1] = hoff[k] + huff[k]->len;
-  }
   const uint8_t *dec = nullptr;
   const uint32_t *slot = nullptr;
   const int32_t *hst = nullptr;
@@ -355,7 +495,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       return NGHTTP2_AMD_ERR_NOMEM;
     E.d_slot = E.d_off + (nh + 1);
     E.d_st = (int32_t *)(E.d_slot + (nh + 1));
-    for (uint32_t k = 0; k < nh; ++k) memcpy(E.h_pool + hoff[k], huff[k]->p, huff[k]->len);
+    parallel_for(nh, 4096, [&](size_t k) { memcpy(E.h_pool + hoff[k], huff[k]->p, huff[k]->len); });
     memset(E.h_pool + hoff[nh], 0, in_bytes - hoff[nh]);
     memcpy(E.h_meta, hoff.data(), (nh + 1) * sizeof(uint32_t));
     if (hipMemcpyAsync(E.d_in, E.h_pool, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -379,128 +519,61 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     hst = h_st;
   }
 
-  // ---- pass 2: blocks in batch order against their inflaters
-  size_t nv_n = 0, ar_n = 0;
-  bool full = false;
-  auto lit_str = [&](const Lit &l, std::string &out) {
-    if (l.huff < 0) {
-      out.assign((const char *)l.p, l.len);
-      return true;
-    }
-    const int32_t s = hst[l.huff];
-    if (s < 0) return false;  // -523: bad padding or EOS (hd_inflate_read_huff, :1740-1750)
-    out.assign((const char *)dec + slot[l.huff], (size_t)s);
-    return true;
-  };
-  auto emit = [&](uint32_t blk, const std::string &name, const std::string &value,
-                  uint8_t flags) {
-    if (nv_n >= nva_cap || ar_n + name.size() + value.size() + 2 > arena_cap) {
-      full = true;
-      return;
-    }
-    nghttp2_amd_hd_nv &o = nva[nv_n++];
-    o.block = blk;
-    o.flags = flags;
-    o.name_off = (uint32_t)ar_n;
-    o.name_len = (uint32_t)name.size();
-    memcpy(arena + ar_n, name.data(), name.size());
-    ar_n += name.size();
-    arena[ar_n++] = 0;  // NUL-terminated like the reference's rcbufs (:2112, :2201)
-    o.value_off = (uint32_t)ar_n;
-    o.value_len = (uint32_t)value.size();
-    memcpy(arena + ar_n, value.data(), value.size());
-    ar_n += value.size();
-    arena[ar_n++] = 0;
-  };
-  auto get = [&](nghttp2_amd_hd_inflater *inf, uint32_t idx, std::string &n, std::string &v) {
-    if (idx < kStaticLen) {
-      n = kStatic[idx][0];
-      v = kStatic[idx][1];
-    } else {
-      n = inf->table[idx - kStaticLen].name;
-      v = inf->table[idx - kStaticLen].value;
-    }
-  };
-  std::string name, value;
-  for (uint32_t i = 0; i < nblocks && !full; ++i) {
-    nghttp2_amd_hd_inflater *inf = inflaters[i];
-    const size_t nv0 = nv_n, ar0 = ar_n;
-    bool ok = !inf->bad;
-    bool head = true;  // size updates only at the head of a block
-    const size_t sv_max = inf->bufsize_max, sv_min = inf->min_max;
-    const bool sv_expect = inf->expect_size;
-    inf->begin_block();
-    for (size_t k = 0; ok && !full && k < bl[i].ops.size(); ++k) {
-      const Op &op = bl[i].ops[k];
-      if (inf->expect_size && op.kind != Op::SIZE) {
-        ok = false;
-        break;
-      }
-      if (op.kind == Op::SIZE) {
-        if (!head || op.value > (inf->min_max < inf->settings_max ? inf->min_max : inf->settings_max)) {
-          ok = false;
-          break;
-        }
-        inf->expect_size = false;
-        inf->min_max = UINT32_MAX;
-        inf->bufsize_max = op.value;
-        inf->shrink();
-        continue;
-      }
-      head = false;
-      if (op.kind == Op::INDEXED) {  // hd_inflate_commit_indexed
-        if (op.value == 0 || op.value > inf->max_index()) {
-          ok = false;
-          break;
-        }
-        get(inf, op.value - 1, name, value);
-        emit(i, name, value, 0);
-        continue;
-      }
-      if (op.new_name) {  // hd_inflate_commit_newname
-        if (!lit_str(op.name, name)) {
-          ok = false;
-          break;
-        }
-      } else {  // hd_inflate_commit_indname
-        if (op.value == 0 || op.value > inf->max_index()) {
-          ok = false;
-          break;
-        }
-        get(inf, op.value - 1, name, value);
-      }
-      if (!lit_str(op.val, value)) {
-        ok = false;
-        break;
-      }
-      if (op.index_required) inf->add(name, value);
-      emit(i, name, value, op.no_index ? 1u : 0u);  // NGHTTP2_NV_FLAG_NO_INDEX
-    }
-    // truncated or malformed wire after the parsed representations; and a
-    // block that ends while a table size update is still expected
-    // (lib/nghttp2_hd.c:2259-2266)
-    if (ok && (!bl[i].parse_ok || inf->expect_size)) ok = false;
-    if (full) {
-      nv_n = nv0;
-      ar_n = ar0;
-      inf->rollback();
-      inf->bufsize_max = sv_max;
-      inf->min_max = sv_min;
-      inf->expect_size = sv_expect;
-      for (uint32_t j = i; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+  // ---- pass 2: each connection's blocks in batch order against its table
+  // (one task per connection), fields into per-block buffers
+  const LitSrc ls{dec, slot, hst};
+  std::unordered_map<nghttp2_amd_hd_inflater *, std::vector<uint32_t>> groups;
+  std::vector<nghttp2_amd_hd_inflater *> conns;
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    auto &g = groups[inflaters[i]];
+    if (g.empty()) conns.push_back(inflaters[i]);
+    g.push_back(i);
+  }
+  // snapshots: a batch that outgrows the caller's buffers is cut at the first
+  // block that does not fit, and the tables replayed up to there
+  std::vector<nghttp2_amd_hd_inflater> snap;
+  snap.reserve(conns.size());
+  for (auto *c : conns) snap.push_back(*c);
+  std::vector<BlockOut> outs(nblocks);
+  parallel_for(conns.size(), 1, [&](size_t c) {
+    for (uint32_t i : groups[conns[c]]) replay_block(conns[c], bl[i], ls, outs[i]);
+  });
+
+  // ---- placement in block order
+  std::vector<size_t> nv_base(nblocks + 1, 0), ar_base(nblocks + 1, 0);
+  uint32_t cut = nblocks;
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    nv_base[i + 1] = nv_base[i] + outs[i].recs.size();
+    ar_base[i + 1] = ar_base[i] + outs[i].bytes.size();
+    if (nv_base[i + 1] > nva_cap || ar_base[i + 1] > arena_cap) {
+      cut = i;
       break;
     }
-    if (!ok) {
-      inf->bad = true;  // sticky (lib/nghttp2_hd.c:1932-1934, :2276)
-      block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
-      // fields emitted before the error stay (the reference emits them one by one)
-    } else {
-      block_status[i] = (int32_t)(nv_n - nv0);
-    }
   }
-  *nva_used = nv_n;
-  *arena_used = ar_n;
-  return full ? NGHTTP2_AMD_ERR_BUFFER_ERROR : 0;
+  if (cut < nblocks) {  // restore, then re-apply the blocks before the cut
+    for (size_t c = 0; c < conns.size(); ++c) *conns[c] = std::move(snap[c]);
+    BlockOut scratch;
+    for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, scratch);
+    for (uint32_t j = cut; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+  }
+  parallel_for(cut, 64, [&](size_t i) {
+    const BlockOut &o = outs[i];
+    const uint32_t ab = (uint32_t)ar_base[i];
+    if (!o.bytes.empty()) memcpy(arena + ab, o.bytes.data(), o.bytes.size());
+    nghttp2_amd_hd_nv *d = nva + nv_base[i];
+    for (size_t k = 0; k < o.recs.size(); ++k) {
+      d[k].block = (uint32_t)i;
+      d[k].name_off = ab + o.recs[k].name_off;
+      d[k].name_len = o.recs[k].name_len;
+      d[k].value_off = ab + o.recs[k].value_off;
+      d[k].value_len = o.recs[k].value_len;
+      d[k].flags = o.recs[k].flags;
+    }
+    block_status[i] = o.status;
+  });
+  *nva_used = nv_base[cut];
+  *arena_used = ar_base[cut];
+  return cut < nblocks ? NGHTTP2_AMD_ERR_BUFFER_ERROR : 0;
 }
 
 }  // extern "C"

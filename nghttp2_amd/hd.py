@@ -335,24 +335,20 @@ class HpackInflater:
         return self.L.nghttp2_amd_hd_inflate_get_dynamic_table_size(self.p)
 
 
-def inflate_blocks(inflaters, blocks, stream=None):
+def inflate_blocks(inflaters, blocks, stream=None, nva_cap=None, arena_cap=None, retry=True):
     """Inflate complete header blocks, block i against inflaters[i], with
     every Huffman literal decoded in one GPU batch.  Returns
-    (status[i], fields[i] = [(name, value, flags)])."""
+    (status[i], fields[i] = [(name, value, flags)]).  A batch that outgrows
+    the field/arena buffers is cut at the first block that does not fit
+    (status NGHTTP2_ERR_BUFFER_ERROR from there on, those blocks not
+    applied); with retry the rest is resubmitted with buffers twice the size."""
     L = _inflate_lib()
     nb = len(blocks)
     bufs = [bytes(b) for b in blocks]
     keep = [ctypes.create_string_buffer(b, max(1, len(b))) for b in bufs]
-    ptrs = (ctypes.c_void_p * max(1, nb))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
-    lens = (ctypes.c_size_t * max(1, nb))(*[len(b) for b in bufs])
-    infs = (ctypes.c_void_p * max(1, nb))(*[i.p.value for i in inflaters])
     total = sum(len(b) for b in bufs)
-    nva_cap = total + 16
-    arena_cap = 8 * total + 64 * (total + 16) + 4096
-    nva = (_Nv * nva_cap)()
-    arena = (ctypes.c_uint8 * arena_cap)()
-    st = (ctypes.c_int32 * max(1, nb))()
-    nv_used, ar_used = ctypes.c_size_t(), ctypes.c_size_t()
+    nva_cap = total + 16 if nva_cap is None else nva_cap
+    arena_cap = 8 * total + 64 * (total + 16) + 4096 if arena_cap is None else arena_cap
     s = None
     if stream is not None:
         s = ctypes.c_void_p(stream.cuda_stream)
@@ -363,17 +359,39 @@ def inflate_blocks(inflaters, blocks, stream=None):
                 s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         except Exception:  # pragma: no cover - torch is part of the image
             s = None
-    rv = L.nghttp2_amd_hd_inflate_blocks(infs, nb, ptrs, lens, nva, nva_cap,
-                                         ctypes.byref(nv_used), arena, arena_cap,
-                                         ctypes.byref(ar_used), st, s)
-    _check(rv, "inflate_blocks")
-    raw = bytes(arena[:ar_used.value])
+    status = [NGHTTP2_ERR_BUFFER_ERROR] * nb
     fields = [[] for _ in range(nb)]
-    for k in range(nv_used.value):
-        r = nva[k]
-        fields[r.block].append((raw[r.name_off:r.name_off + r.name_len],
-                                raw[r.value_off:r.value_off + r.value_len], r.flags))
-    return [st[i] for i in range(nb)], fields
+    first = 0
+    while first < nb:
+        m = nb - first
+        ptrs = (ctypes.c_void_p * m)(*[ctypes.cast(k, ctypes.c_void_p) for k in keep[first:]])
+        lens = (ctypes.c_size_t * m)(*[len(b) for b in bufs[first:]])
+        infs = (ctypes.c_void_p * m)(*[i.p.value for i in inflaters[first:]])
+        nva = (_Nv * max(1, nva_cap))()
+        arena = (ctypes.c_uint8 * max(1, arena_cap))()
+        st = (ctypes.c_int32 * m)()
+        nv_used, ar_used = ctypes.c_size_t(), ctypes.c_size_t()
+        rv = L.nghttp2_amd_hd_inflate_blocks(infs, m, ptrs, lens, nva, nva_cap,
+                                             ctypes.byref(nv_used), arena, arena_cap,
+                                             ctypes.byref(ar_used), st, s)
+        if rv != NGHTTP2_ERR_BUFFER_ERROR:
+            _check(rv, "inflate_blocks")
+        raw = bytes(arena[:ar_used.value])
+        for k in range(nv_used.value):
+            r = nva[k]
+            fields[first + r.block].append((raw[r.name_off:r.name_off + r.name_len],
+                                            raw[r.value_off:r.value_off + r.value_len], r.flags))
+        done = 0
+        while done < m and st[done] != NGHTTP2_ERR_BUFFER_ERROR:
+            status[first + done] = st[done]
+            done += 1
+        first += done
+        if done < m:
+            if not retry:
+                break
+            if done == 0:
+                nva_cap, arena_cap = 2 * nva_cap + 16, 2 * arena_cap + 4096
+    return status, fields
 
 
 # ---------------------------------------------------------------------------

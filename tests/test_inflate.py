@@ -126,7 +126,7 @@ def test_expected_table_size_update_cpu():
 
 
 # ---- random batches (GPU: Huffman literals) ----
-def _encode_block(rng, table, fields, table_max):
+def _encode_block(rng, table, fields, table_max, huff_p=0.7):
     """A small HPACK encoder for test blocks: random representation and
     Huffman choices.  `table` mirrors the decoder's dynamic table."""
     out = bytearray()
@@ -135,7 +135,7 @@ def _encode_block(rng, table, fields, table_max):
         out.extend(O.encode_length(v, prefix, first))
 
     def string(s):
-        if rng.random() < 0.7:
+        if rng.random() < huff_p:
             out.extend(O.emit_string(s))
         else:  # raw even when Huffman would be shorter
             integer(len(s), 7, 0)
@@ -219,3 +219,57 @@ def test_inflate_random_connections_vs_oracle():
         assert (st[k], f[k]) == (rs, rf), (k, c)
     for c in range(nconn):
         assert infs[c].dynamic_table() == [tuple(e) for e in refs[c].table]
+
+
+# ---- many connections without Huffman literals (no GPU call): the threaded
+# replay, and the buffer cut with its table rollback ----
+def _plain_batch(seed, nconn, nblk):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    enc_tables = [[] for _ in range(nconn)]
+    order, blocks = [], []
+    for _ in range(nblk):
+        for c in rng.permutation(nconn):
+            fields = _random_fields(rng, int(rng.integers(1, 10)))
+            blk = _encode_block(rng, enc_tables[c], fields, 4096, huff_p=0.0)
+            if rng.random() < 0.05:
+                blk = blk[:max(1, len(blk) - int(rng.integers(1, 4)))]
+            order.append(int(c))
+            blocks.append(blk)
+    return order, blocks
+
+
+def test_inflate_many_connections_plain_cpu():
+    import nghttp2_amd
+    nconn = 300
+    order, blocks = _plain_batch(0xC0FFEE, nconn, 4)
+    infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+    refs = [HO.Inflater() for _ in range(nconn)]
+    st, f = nghttp2_amd.inflate_blocks([infs[c] for c in order], blocks)
+    for k, (c, blk) in enumerate(zip(order, blocks)):
+        assert (st[k], f[k]) == refs[c].inflate_block(blk), (k, c)
+    for c in range(nconn):
+        assert infs[c].dynamic_table() == [tuple(e) for e in refs[c].table]
+
+
+def test_inflate_buffer_cut_rolls_back_cpu():
+    """Buffers too small for the batch: the blocks before the cut are applied,
+    the rest are not (tables as if they never came), and resubmitting them
+    gives the oracle's result."""
+    import nghttp2_amd
+    from nghttp2_amd import hd
+    nconn = 40
+    order, blocks = _plain_batch(0xB0F, nconn, 5)
+    infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+    refs = [HO.Inflater() for _ in range(nconn)]
+    st, f = nghttp2_amd.inflate_blocks([infs[c] for c in order], blocks, arena_cap=6000, retry=False)
+    cut = st.index(hd.NGHTTP2_ERR_BUFFER_ERROR)
+    assert 0 < cut < len(blocks)
+    assert all(s == hd.NGHTTP2_ERR_BUFFER_ERROR for s in st[cut:])
+    for k in range(cut):
+        assert (st[k], f[k]) == refs[order[k]].inflate_block(blocks[k]), k
+    for c in range(nconn):
+        assert infs[c].dynamic_table() == [tuple(e) for e in refs[c].table], c
+    st2, f2 = nghttp2_amd.inflate_blocks([infs[c] for c in order[cut:]], blocks[cut:],
+                                         arena_cap=6000)
+    for k in range(cut, len(blocks)):
+        assert (st2[k - cut], f2[k - cut]) == refs[order[k]].inflate_block(blocks[k]), k
