@@ -274,6 +274,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   // ---- pass 1: representations; one task per connection, its lists in
   // batch order (connections are independent)
   using nghttp2_amd_host::parallel_for;
+  nghttp2_amd_host::Phases ph("deflate");
   std::vector<std::vector<Piece>> pieces(nblocks);
   std::vector<std::vector<std::pair<const uint8_t *, uint32_t>>> blits(nblocks);
   auto deflate_list = [&](uint32_t i) {
@@ -393,6 +394,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     rawbase[i + 1] = rawbase[i] + r;
   }
 
+  ph.mark("tables");
   // ---- GPU: frame every literal of the batch (emit_string)
   const uint32_t nl = litbase[nblocks];
   std::lock_guard<std::mutex> guard(engine().mu);
@@ -415,7 +417,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
         !grow_dev((void **)&E.d_off, &E.doff_cap, 2u * ((size_t)nl + 1u) * sizeof(uint32_t)))
       return NGHTTP2_AMD_ERR_NOMEM;
     // the literal pool and its offsets, block by block
-    parallel_for(nblocks, 64, [&](size_t i) {
+    parallel_for(nblocks, 256, [&](size_t i) {
       uint32_t o = (uint32_t)rawbase[i];
       uint32_t k = litbase[i];
       for (auto &l : blits[i]) {
@@ -444,10 +446,11 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     froff = h_fo;
   }
 
+  ph.mark("gpu");
   // ---- pass 2: each block's wire size, placement in block order, then the
   // bytes (representation bytes and framed literals, in order)
   std::vector<size_t> need(nblocks, 0);
-  parallel_for(nblocks, 64, [&](size_t i) {
+  parallel_for(nblocks, 256, [&](size_t i) {
     size_t n = 0;
     for (const Piece &pc : pieces[i]) {
       n += pc.bytes.size();
@@ -478,7 +481,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     }
     out_off[i + 1] = (uint32_t)o;
   }
-  parallel_for(nblocks, 64, [&](size_t i) {
+  parallel_for(nblocks, 256, [&](size_t i) {
     if (block_status[i] < 0) return;
     uint8_t *w = out + out_off[i];
     for (const Piece &pc : pieces[i]) {
@@ -493,6 +496,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
       }
     }
   });
+  ph.mark("wire");
   return ret;
 }
 

@@ -445,9 +445,10 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
 
   // ---- pass 1: parse every block (stateless: one task per block)
   using nghttp2_amd_host::parallel_for;
+  nghttp2_amd_host::Phases ph("inflate");
   std::vector<Block> bl(nblocks);
   std::vector<uint32_t> nhuff(nblocks + 1, 0);  // Huffman literals per block, then prefix
-  parallel_for(nblocks, 16, [&](size_t i) {
+  parallel_for(nblocks, 64, [&](size_t i) {
     // a malformed block keeps the representations before the error: the
     // reference emits those fields before it fails
     bl[i].parse_ok = parse_block(blocks[i], block_lens[i], bl[i]);
@@ -476,6 +477,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   }
   for (uint32_t k = 0; k < nh; ++k) hoff[k + 1] = hoff[k] + huff[k]->len;
 
+  ph.mark("parse");
   // ---- GPU: every Huffman literal of the batch in one decode
   std::lock_guard<std::mutex> guard(engine().mu);
   Engine &E = engine();
@@ -519,6 +521,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     hst = h_st;
   }
 
+  ph.mark("gpu");
   // ---- pass 2: each connection's blocks in batch order against its table
   // (one task per connection), fields into per-block buffers
   const LitSrc ls{dec, slot, hst};
@@ -539,6 +542,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     for (uint32_t i : groups[conns[c]]) replay_block(conns[c], bl[i], ls, outs[i]);
   });
 
+  ph.mark("replay");
   // ---- placement in block order
   std::vector<size_t> nv_base(nblocks + 1, 0), ar_base(nblocks + 1, 0);
   uint32_t cut = nblocks;
@@ -556,7 +560,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, scratch);
     for (uint32_t j = cut; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
   }
-  parallel_for(cut, 64, [&](size_t i) {
+  parallel_for(cut, 256, [&](size_t i) {
     const BlockOut &o = outs[i];
     const uint32_t ab = (uint32_t)ar_base[i];
     if (!o.bytes.empty()) memcpy(arena + ab, o.bytes.data(), o.bytes.size());
@@ -571,6 +575,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     }
     block_status[i] = o.status;
   });
+  ph.mark("place");
   *nva_used = nv_base[cut];
   *arena_used = ar_base[cut];
   return cut < nblocks ? NGHTTP2_AMD_ERR_BUFFER_ERROR : 0;

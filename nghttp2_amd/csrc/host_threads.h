@@ -3,16 +3,23 @@
 // The inflate/deflate front-ends (hd_inflate.cpp, hd_deflate.cpp) do their
 // table work per connection, and connections are independent, so a batch of
 // many connections spreads over host threads: one task per connection, or per
-// block for the stateless parse.  Threads are started per call (a call is
-// a whole batch) and only when there are enough tasks to pay for them.
-// NGHTTP2_AMD_HOST_THREADS overrides the count; the default is the hardware
+// block for the stateless parse.  The workers are started once per process
+// and parked between calls; a call hands them a job and works on it itself.
+// NGHTTP2_AMD_HOST_THREADS sets the count; the default is the hardware
 // threads, capped at 16 (the host share of one GPU on the MI355X boxes).
+// NGHTTP2_AMD_TRACE=1 prints each call's phase times to stderr.
 #pragma once
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
 #include <system_error>
 #include <thread>
 #include <vector>
@@ -29,19 +36,75 @@ inline unsigned host_threads() {
   return t;
 }
 
+class Pool {
+ public:
+  static Pool &get() {
+    static Pool *p = new Pool(host_threads() - 1);  // never destroyed: workers park until exit
+    return *p;
+  }
+  unsigned workers() const { return (unsigned)th_.size(); }
+  // Runs fn on every worker and on the caller; returns when all are done.
+  // Calls from several host threads take turns.
+  void run(const std::function<void()> &fn) {
+    std::lock_guard<std::mutex> turn(run_mu_);
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      job_ = &fn;
+      active_ = (unsigned)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn();
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  explicit Pool(unsigned n) {
+    for (unsigned k = 0; k < n; ++k) {
+      try {
+        th_.emplace_back([this] { loop(); });
+        th_.back().detach();
+      } catch (const std::system_error &) {
+        break;
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void()> *j;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_ != seen; });
+        seen = gen_;
+        j = job_;
+      }
+      (*j)();
+      std::lock_guard<std::mutex> l(mu_);
+      if (--active_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void()> *job_ = nullptr;
+  unsigned active_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // f(i) for i in [0, n), `grain` consecutive indices per fetch; serial when
-// fewer than 2 * grain tasks or one thread.
+// there are fewer than two grains of work.
 template <class F>
 void parallel_for(size_t n, size_t grain, F &&f) {
   if (grain == 0) grain = 1;
-  const size_t chunks = (n + grain - 1) / grain;
-  const unsigned t = (unsigned)std::min<size_t>(host_threads(), chunks);
-  if (t <= 1) {
+  if (n < 2 * grain || host_threads() <= 1) {
     for (size_t i = 0; i < n; ++i) f(i);
     return;
   }
   std::atomic<size_t> next{0};
-  auto work = [&]() {
+  const std::function<void()> work = [&]() {
     for (;;) {
       const size_t a = next.fetch_add(grain, std::memory_order_relaxed);
       if (a >= n) return;
@@ -49,15 +112,35 @@ void parallel_for(size_t n, size_t grain, F &&f) {
       for (size_t i = a; i < b; ++i) f(i);
     }
   };
-  std::vector<std::thread> th;
-  th.reserve(t - 1);
-  try {
-    for (unsigned k = 1; k < t; ++k) th.emplace_back(work);
-  } catch (const std::system_error &) {
-    // fewer threads than asked: the ones started and this one finish the work
-  }
-  work();
-  for (auto &x : th) x.join();
+  Pool::get().run(work);
 }
+
+inline bool trace_on() {
+  static const bool on = getenv("NGHTTP2_AMD_TRACE") != nullptr;
+  return on;
+}
+
+// Phase times of one call, printed at the end of the call when tracing.
+class Phases {
+ public:
+  explicit Phases(const char *who) : who_(who), on_(trace_on()), t_(std::chrono::steady_clock::now()) {}
+  void mark(const char *name) {
+    if (!on_) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[96];
+    snprintf(b, sizeof b, " %s=%.1fus", name, std::chrono::duration<double, std::micro>(now - t_).count());
+    log_ += b;
+    t_ = now;
+  }
+  ~Phases() {
+    if (on_) fprintf(stderr, "[nghttp2_amd %s]%s\n", who_, log_.c_str());
+  }
+
+ private:
+  const char *who_;
+  bool on_;
+  std::chrono::steady_clock::time_point t_;
+  std::string log_;
+};
 
 }  // namespace nghttp2_amd_host

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -50,7 +51,10 @@ struct Case {
   bool comma_after = false;
   size_t old_max = 0, new_max = 0;  // max dynamic table size before / after
   int32_t status = 0;
-  std::vector<std::pair<std::string, std::string>> fields;
+  // the case's fields: nv[0..nnv) into arena (buffers of its batch call)
+  const nghttp2_amd_hd_nv *nv = nullptr;
+  size_t nnv = 0;
+  const uint8_t *arena = nullptr;
   jl::Ptr table;
   bool done = false;
   bool skipped = false;  // header_table_size could not be applied
@@ -144,9 +148,17 @@ void read_json(Conn &c, const std::string &text) {
   }
 }
 
+// The buffers of every call of a run (the cases point into them).
+struct CallBufs {
+  std::unique_ptr<nghttp2_amd_hd_nv[]> nva;
+  std::unique_ptr<uint8_t[]> arena;
+};
+std::vector<CallBufs> g_bufs;
+
 // One batched inflate call over (connection, case) pairs; the caller's
 // buffers grow until everything fits (a block that does not fit is not
-// applied, so the rest is simply resubmitted).
+// applied, so the rest is simply resubmitted).  Buffers are left
+// uninitialised: the library writes what it reports.
 double run_batch(std::vector<std::pair<Conn *, Case *>> &batch) {
   if (batch.empty()) return 0;
   const auto t0 = std::chrono::steady_clock::now();
@@ -155,24 +167,28 @@ double run_batch(std::vector<std::pair<Conn *, Case *>> &batch) {
   size_t nva_cap = wire + batch.size() + 16;
   size_t arena_cap = 16 * wire + 4096;
   size_t first = 0;
-  std::vector<nghttp2_amd_hd_nv> nva;
-  std::vector<uint8_t> arena;
+  std::vector<nghttp2_amd_hd_inflater *> infs;
+  std::vector<const uint8_t *> ptrs;
+  std::vector<size_t> lens;
+  std::vector<int32_t> st;
   while (first < batch.size()) {
     const uint32_t nb = (uint32_t)(batch.size() - first);
-    std::vector<nghttp2_amd_hd_inflater *> infs(nb);
-    std::vector<const uint8_t *> ptrs(nb);
-    std::vector<size_t> lens(nb);
-    std::vector<int32_t> st(nb);
+    infs.resize(nb);
+    ptrs.resize(nb);
+    lens.resize(nb);
+    st.resize(nb);
     for (uint32_t j = 0; j < nb; ++j) {
       infs[j] = batch[first + j].first->inf;
       ptrs[j] = batch[first + j].second->bytes.data();
       lens[j] = batch[first + j].second->bytes.size();
     }
-    nva.resize(nva_cap);
-    arena.resize(arena_cap);
+    CallBufs cb;
+    cb.nva.reset(new nghttp2_amd_hd_nv[nva_cap]);
+    cb.arena.reset(new uint8_t[arena_cap]);
     size_t nv_used = 0, ar_used = 0;
-    const int rv = nghttp2_amd_hd_inflate_blocks(infs.data(), nb, ptrs.data(), lens.data(), nva.data(), nva_cap,
-                                                 &nv_used, arena.data(), arena_cap, &ar_used, st.data(), nullptr);
+    const int rv = nghttp2_amd_hd_inflate_blocks(infs.data(), nb, ptrs.data(), lens.data(), cb.nva.get(),
+                                                 nva_cap, &nv_used, cb.arena.get(), arena_cap, &ar_used,
+                                                 st.data(), nullptr);
     if (rv < 0 && rv != NGHTTP2_AMD_ERR_BUFFER_ERROR) die("inflate failed with error code " + std::to_string(rv));
     size_t f = 0;
     uint32_t j = 0;
@@ -180,10 +196,12 @@ double run_batch(std::vector<std::pair<Conn *, Case *>> &batch) {
       Case &k = *batch[first + j].second;
       k.status = st[j];
       k.done = true;
-      for (; f < nv_used && nva[f].block == j; ++f)
-        k.fields.emplace_back(std::string((const char *)arena.data() + nva[f].name_off),  // C string, as dump_header
-                              std::string((const char *)arena.data() + nva[f].value_off, nva[f].value_len));
+      k.nv = cb.nva.get() + f;
+      k.arena = cb.arena.get();
+      while (f < nv_used && cb.nva[f].block == j) ++f;
+      k.nnv = (size_t)(cb.nva.get() + f - k.nv);
     }
+    g_bufs.push_back(std::move(cb));
     if (j == 0) {  // not even the first block fit
       nva_cap *= 2;
       arena_cap *= 2;
@@ -250,11 +268,13 @@ int main(int argc, char **argv) {
   auto run_all = [&]() -> double {  // fresh inflaters, every case decoded once
     double secs = 0;
     nblocks = wire_bytes = 0;
+    g_bufs.clear();
     for (auto &c : conns) {
       if (c.inf) nghttp2_amd_hd_inflate_del(c.inf);
       if (nghttp2_amd_hd_inflate_new(&c.inf) != 0) die("inflate_new failed");
       for (auto &k : c.cases) {
-        k.fields.clear();
+        k.nv = nullptr;
+        k.nnv = 0;
         k.status = 0;
         k.done = k.skipped = false;
         k.table.reset();
@@ -322,12 +342,15 @@ int main(int argc, char **argv) {
       obj->set("seq", jl::integer(k.seq));
       obj->set("wire", jl::string(k.wire->s));
       auto hs = jl::make(jl::Value::ARR);
-      for (auto &f : k.fields) {
+      for (size_t q = 0; q < k.nnv; ++q) {
+        const nghttp2_amd_hd_nv &f = k.nv[q];
         auto p = jl::make(jl::Value::OBJ);
-        p->set(f.first, jl::string(f.second));
+        // the name as a C string, as dump_header (src/comp_helper.c:98-110) takes it
+        p->set(std::string((const char *)k.arena + f.name_off),
+               jl::string(std::string((const char *)k.arena + f.value_off, f.value_len)));
         hs->arr.push_back(p);
       }
-      fields += k.fields.size();
+      fields += k.nnv;
       obj->set("headers", hs);
       if (k.old_max != k.new_max) obj->set("header_table_size", jl::integer((int64_t)k.new_max));
       if (k.table) obj->set("header_table", k.table);
