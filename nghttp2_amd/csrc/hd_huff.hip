@@ -720,15 +720,15 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
 
 // ---------------------------------------------------------------------------
 // Item decoding (DESIGN.md "decode").  A string of E encoded bytes is cut
-// into m = max(1, ceil(E / 64)) ITEMS:
+// into m = max(1, ceil(E / P)) ITEMS, P = PIECE_BYTES = 64:
 //   item (i, 0)   the string from its first bit (exact), up to the first
-//                 codeword boundary at or after byte sa[i] + 64, or its end;
-//   item (i, k>0) the piece from byte sa[i] + 64 k: a speculative entry
+//                 codeword boundary at or after byte sa[i] + P, or its end;
+//   item (i, k>0) the piece from byte sa[i] + P k: a speculative entry
 //                 (warm-up from SUB_OV bytes early to the first boundary >=
 //                 the piece start), then on to the first boundary >= piece
-//                 start + 64, or the string end.
+//                 start + P, or the string end.
 // A wave takes 64 consecutive items per round (one per lane); their input
-// bytes are contiguous (<= 64 * 64 + warm-up) and are staged once in the
+// bytes are contiguous (<= 64 P + warm-up) and are staged once in the
 // wave's LDS region (coalesced 16-byte loads, byte-swapped to big-endian
 // words).  An item's entry is verified against the previous lane's exit (or
 // the carry from the previous round); mismatches are re-decoded from the
@@ -742,7 +742,12 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
 #endif
 #define DEC_NT (WAVE * DEC_WAVES)
 #define TASK_STR 64                                // strings per wave task
-#define PIECE_BYTES 64u                            // input bytes per item (string piece)
+#ifndef PIECE_BYTES
+// input bytes per item (string piece).  80 decodes config 3 in 558 us against
+// 586 us isolated, but its 150 KB of LDS keeps encode workgroups off the CU
+// in the 2-stream bench (900 vs 906 GB/s, tools/diag/ab_bench.sh)
+#define PIECE_BYTES 64u
+#endif
 #ifndef SUB_OV
 #define SUB_OV 24u                                 // warm-up bytes of a k > 0 piece
 #endif

@@ -40,7 +40,8 @@ def lib():
     """Load the HIP library; raises if it was not built (no fallback)."""
     global _lib
     if _lib is None:
-        path = lib_path()
+        # NGHTTP2_AMD_LIB: an ablation build of the same library (tools/diag)
+        path = os.environ.get("NGHTTP2_AMD_LIB") or lib_path()
         if not os.path.exists(path):
             raise RuntimeError(
                 "nghttp2_amd: HIP library %s is missing -- run "

@@ -15,7 +15,7 @@ codec = nghttp2_amd.HuffmanBatchCodec(dev)
 src = torch.from_numpy(pool).to(dev); so = torch.from_numpy(off.view(np.int32)).to(dev)
 enc, eo = codec.encode(src, so, raw_bytes=int(off[-1])); torch.cuda.synchronize()
 E = int(eo[-1].item()); n = len(off) - 1
-L = ctypes.CDLL(os.path.join(HERE, "lib_stamps.so"), mode=ctypes.RTLD_LOCAL)
+L = ctypes.CDLL(os.path.join(HERE, os.environ.get("STAMPS_LIB", "lib_stamps.so")), mode=ctypes.RTLD_LOCAL)
 vp = ctypes.c_void_p
 L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]
 cap = codec.decode_bound(E, n)

@@ -57,8 +57,15 @@ for rnd in range(10):
         a.record(s); run_enc(L); b.record(s); torch.cuda.synchronize()
         eres[k].append(a.elapsed_time(b) * 1000)
 res = {k: [] for k in libs}
+ref_dec = None
 for k, L in libs.items():
+    dst.zero_(); st.zero_()
     for _ in range(3): run(L)
+    torch.cuda.synchronize()
+    if ref_dec is None:
+        ref_dec = (dst.clone(), st.clone(), doff.clone())
+    else:
+        assert torch.equal(dst, ref_dec[0]) and torch.equal(st, ref_dec[1]) and torch.equal(doff, ref_dec[2]), k + ": decode differs"
 torch.cuda.synchronize()
 for rnd in range(10):
     for k, L in libs.items():
