@@ -223,6 +223,33 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_fsm_batch(const uint8_t *src, 
                                          void *stream);
 
 /* ------------------------------------------------------------------ */
+/* Header-name tokens and name hash              */
+/* ------------------------------------------------------------------ */
+/*
+ * Replaces lookup_token (lib/nghttp2_hd.c:137-520) and name_hash
+ * (lib/nghttp2_hd.c:536-547), both static in the reference and called per
+ * header field by deflate_nv (:1388-1393) and the inflater (:1811).
+ *
+ * nghttp2_amd_hd_name_tokens_batch: N names in the batch layout (device pool
+ * + uint32 offsets[N+1], pool readable to align_up(off[N], 16) + 16);
+ * token[i] = lookup_token(name i) (-1, or NGHTTP2_TOKEN_* of
+ * lib/nghttp2_hd.h:56-116: the first static-table index of a static name,
+ * 61..67 for te, connection, keep-alive, proxy-connection, upgrade,
+ * :protocol, priority); hash[i] = 32-bit FNV-1a of name i (equal to the
+ * reference's static_table[token].hash for a static name).  Device pointers,
+ * asynchronous on `stream`.
+ *
+ * nghttp2_amd_hd_lookup_token / nghttp2_amd_hd_name_hash: the same for one
+ * host name (what a single deflate_nv call binds).
+ */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_name_tokens_batch(const uint8_t *names,
+                                                        const uint32_t *name_off, uint32_t n,
+                                                        int32_t *token, uint32_t *hash,
+                                                        void *stream);
+NGHTTP2_AMD_EXTERN int32_t nghttp2_amd_hd_lookup_token(const uint8_t *name, size_t namelen);
+NGHTTP2_AMD_EXTERN uint32_t nghttp2_amd_hd_name_hash(const uint8_t *name, size_t namelen);
+
+/* ------------------------------------------------------------------ */
 /* Batched HPACK inflate front-end               */
 /* ------------------------------------------------------------------ */
 /*

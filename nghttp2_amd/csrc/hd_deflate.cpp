@@ -31,6 +31,7 @@
 
 #include "../../include/nghttp2_amd_hd.h"
 #include "host_threads.h"
+#include "hd_tokens.h"
 
 namespace {
 
@@ -56,37 +57,14 @@ const char *const kStatic[kStaticLen][2] = {
 
 enum Mode { WITH_INDEXING, WITHOUT_INDEXING, NEVER_INDEXING };  // nghttp2_hd.h
 
-// lookup_token (lib/nghttp2_hd.c:137) restricted to what the deflater uses:
-// the first static-table index of a static name, else -1 (other tokens only
-// stand for name equality in the table search).
-size_t static_name_len(uint32_t i) {
-  static size_t lens[kStaticLen];
-  static bool init = [] {
-    for (uint32_t k = 0; k < kStaticLen; ++k) lens[k] = strlen(kStatic[k][0]);
-    return true;
-  }();
-  (void)init;
-  return lens[i];
-}
-int32_t static_token(const uint8_t *name, size_t len) {
-  for (uint32_t i = 0; i < kStaticLen; ++i)
-    if (static_name_len(i) == len && memcmp(kStatic[i][0], name, len) == 0) return (int32_t)i;
-  return -1;
-}
 bool name_is(const uint8_t *name, size_t len, const char *s) {
   return strlen(s) == len && memcmp(s, name, len) == 0;
 }
 
-// FNV-1a of a name (the reference's name_hash, lib/nghttp2_hd.c:536-547):
-// the table search compares it before the bytes.
-uint32_t name_hash(const uint8_t *p, size_t n) {
-  uint32_t h = 2166136261u;
-  for (size_t i = 0; i < n; ++i) {
-    h ^= p[i];
-    h *= 16777619u;
-  }
-  return h;
-}
+// lookup_token (lib/nghttp2_hd.c:137) and name_hash (:536-547): one FNV-1a
+// pass and a hashed probe (hd_tokens.h), shared with the GPU kernel.
+using hdtok::name_hash;
+constexpr int32_t kLastStaticToken = 60;  // NGHTTP2_TOKEN_WWW_AUTHENTICATE
 
 struct Entry {
   std::string name, value;
@@ -301,22 +279,19 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     }
     for (uint32_t k = block_nv_off[i]; k < block_nv_off[i + 1]; ++k) {
       const nghttp2_amd_nv &nv = nva[k];
-      const int32_t token = static_token(nv.name, nv.namelen);
       const uint32_t nh = name_hash(nv.name, nv.namelen);
+      const int32_t token = hdtok::lookup_token(nv.name, nv.namelen, nh);
       const size_t room = nv.namelen + nv.valuelen + kEntryOverhead;
       // deflate_nv (:1373-1400): never-index authorization, short cookies
       // and fields flagged NO_INDEX; hd_deflate_decide_indexing (:1358-1371)
       Mode mode;
-      if (name_is(nv.name, nv.namelen, "authorization") ||
-          (name_is(nv.name, nv.namelen, "cookie") && nv.valuelen < 20) || (nv.flags & 1u)) {
+      if (token == 22 /* authorization */ || (token == 31 /* cookie */ && nv.valuelen < 20) ||
+          (nv.flags & 1u)) {
         mode = NEVER_INDEXING;
-      } else if (name_is(nv.name, nv.namelen, ":path") || name_is(nv.name, nv.namelen, "age") ||
-                 name_is(nv.name, nv.namelen, "content-length") ||
-                 name_is(nv.name, nv.namelen, "etag") ||
-                 name_is(nv.name, nv.namelen, "if-modified-since") ||
-                 name_is(nv.name, nv.namelen, "if-none-match") ||
-                 name_is(nv.name, nv.namelen, "location") ||
-                 name_is(nv.name, nv.namelen, "set-cookie") || room > d->bufsize_max * 3 / 4) {
+      } else if (token == 3 /* :path */ || token == 20 /* age */ || token == 27 /* content-length */ ||
+                 token == 33 /* etag */ || token == 39 /* if-modified-since */ ||
+                 token == 40 /* if-none-match */ || token == 45 /* location */ ||
+                 token == 54 /* set-cookie */ || room > d->bufsize_max * 3 / 4) {
         mode = WITHOUT_INDEXING;
       } else {
         mode = WITH_INDEXING;
@@ -342,7 +317,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
           break;
         }
       }
-      if (!exact && token >= 0) {  // search_static_table (:1201-1223)
+      if (!exact && token >= 0 && token <= kLastStaticToken) {  // search_static_table (:1201-1223)
         idx = token;
         if (!name_only) {
           for (uint32_t s = (uint32_t)token; s < kStaticLen && name_is(nv.name, nv.namelen, kStatic[s][0]); ++s) {

@@ -1,0 +1,139 @@
+// hd_names.hip -- batched header-name tokenisation and FNV-1a name hash
+//  for gfx950.
+//
+// Reference: lookup_token (lib/nghttp2_hd.c:137-520) and name_hash
+// (:536-547), called once per header field by deflate_nv (:1388-1393) and by
+// the inflater (:1811).  Here a batch of N names in SoA form (byte pool +
+// uint32 offsets[N+1], the Huffman batch layout) gives token[N] (int32,
+// lookup_token's result: -1 or NGHTTP2_TOKEN_*) and hash[N] (FNV-1a of the
+// name, which equals static_table[token].hash for a static name).
+//
+// Layout and bound: one lane per name.  FNV-1a is a serial chain per name, so
+// each lane walks its own name in 32-byte chunks of aligned 16-byte loads
+// (the next chunk in flight while the current one is hashed, branch-free
+// predicated steps); the 64 names of a wave are contiguous in the pool, so
+// their loads share cache lines and HBM sees each byte once.  The 128-slot
+// token table (hd_tokens.h) is staged in LDS once per workgroup (1.6 KB);
+// a hash + length hit is verified with dword compares.  HBM traffic per
+// name: its bytes + 4 (offset) in, 8 out -- an HBM-bound byte scan, no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/nghttp2_amd_hd.h"
+#include "hd_tokens.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+constexpr uint32_t NT_WG = 256;
+
+__constant__ hdtok::Table kTokTable = hdtok::kTable;
+
+__global__ __launch_bounds__(NT_WG) void k_name_tokens(const uint8_t *__restrict__ names,
+                                                       const uint32_t *__restrict__ off, uint32_t n,
+                                                       int32_t *__restrict__ token,
+                                                       uint32_t *__restrict__ hash) {
+  __shared__ uint32_t th[hdtok::kSlots], tm[hdtok::kSlots];
+  __shared__ uint32_t tn[hdtok::kNameBytes / 4];
+  for (uint32_t i = threadIdx.x; i < hdtok::kSlots; i += NT_WG) {
+    th[i] = kTokTable.hash[i];
+    tm[i] = kTokTable.meta[i];
+  }
+  for (uint32_t i = threadIdx.x; i < hdtok::kNameBytes / 4; i += NT_WG)
+    tn[i] = reinterpret_cast<const uint32_t *>(kTokTable.names)[i];
+  __syncthreads();  // the only workgroup barrier
+  const lds_u32 *TH = (const lds_u32 *)th, *TM = (const lds_u32 *)tm, *TN = (const lds_u32 *)tn;
+  const uint32_t s = blockIdx.x * NT_WG + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t a = off[s], b = off[s + 1], len = b - a;
+  // FNV-1a over 32-byte chunks from the 16-byte aligned base below the name,
+  // the next chunk's loads issued before the current chunk is hashed
+  const uint4 *g = reinterpret_cast<const uint4 *>(names);
+  uint32_t h = hdtok::kFnvBasis;
+  uint32_t cb = a & ~15u;
+  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
+  if (a < b) {
+    c0 = g[cb >> 4];
+    c1 = g[(cb >> 4) + 1u];
+  }
+  for (; cb < b; cb += 32u) {
+    uint4 n0 = c0, n1 = c1;
+    if (cb + 32u < b) {
+      n0 = g[(cb >> 4) + 2u];
+      n1 = g[(cb >> 4) + 3u];
+    }
+    const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 32u; ++j) {
+      const uint32_t p = cb + j;
+      const uint32_t c = (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+      const uint32_t hn = (h ^ c) * hdtok::kFnvPrime;
+      h = (p >= a && p < b) ? hn : h;
+    }
+    c0 = n0;
+    c1 = n1;
+  }
+  // token: probe by hash, verify length and bytes (aligned dword loads of
+  // the name, realigned with v_alignbyte; table names are dword aligned and
+  // zero padded)
+  int32_t tok = -1;
+  if (len <= 32u) {
+    for (uint32_t slot = h & (hdtok::kSlots - 1u), k = 0; k < hdtok::kSlots;
+         ++k, slot = (slot + 1u) & (hdtok::kSlots - 1u)) {
+      const uint32_t m = TM[slot];
+      if (m == 0) break;
+      if (TH[slot] != h || hdtok::meta_len(m) != len) continue;
+      const uint32_t *gw = reinterpret_cast<const uint32_t *>(names + (a & ~3u));
+      const uint32_t sh = a & 3u, nw = (sh + len + 3u) >> 2;  // aligned words holding the name
+      uint32_t d[9];
+#pragma unroll
+      for (uint32_t i = 0; i < 9u; ++i) d[i] = i < nw ? gw[i] : 0u;
+      const lds_u32 *q = TN + (hdtok::meta_off(m) >> 2);
+      bool eq = true;
+#pragma unroll
+      for (uint32_t i = 0; i < 8u; ++i) {
+        if (4u * i >= len) break;
+        uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        const uint32_t left = len - 4u * i;
+        if (left < 4u) v &= (1u << (8u * left)) - 1u;
+        eq = eq && v == q[i];
+      }
+      if (eq) {
+        tok = (int32_t)hdtok::meta_token(m);
+        break;
+      }
+    }
+  }
+  token[s] = tok;
+  hash[s] = h;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nghttp2_amd_hd_name_tokens_batch(const uint8_t *names, const uint32_t *name_off, uint32_t n,
+                                     int32_t *token, uint32_t *hash, void *stream) {
+  if (n == 0) return 0;
+  if (!names || !name_off || !token || !hash) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(k_name_tokens, dim3((n + NT_WG - 1u) / NT_WG), dim3(NT_WG), 0,
+                     (hipStream_t)stream, names, name_off, n, token, hash);
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  fprintf(stderr, "nghttp2_amd_hd: HIP error %s\n", hipGetErrorString(e));
+  return NGHTTP2_AMD_ERR_FATAL;
+}
+
+int32_t nghttp2_amd_hd_lookup_token(const uint8_t *name, size_t namelen) {
+  if (!name && namelen) return -1;
+  return hdtok::lookup_token(name, namelen, hdtok::name_hash(name, namelen));
+}
+
+uint32_t nghttp2_amd_hd_name_hash(const uint8_t *name, size_t namelen) {
+  if (!name) return hdtok::kFnvBasis;
+  return hdtok::name_hash(name, namelen);
+}
+
+}  // extern "C"

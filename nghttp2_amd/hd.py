@@ -77,8 +77,25 @@ def lib():
         L.nghttp2_amd_hd_emit_strings_workspace_size.restype = sz
         L.nghttp2_amd_hd_emit_strings_workspace_size.argtypes = [u64, u32]
         L.nghttp2_amd_hd_emit_strings_batch.argtypes = [vp, vp, u32, u64, vp, sz, vp, vp, sz, vp]
+        L.nghttp2_amd_hd_name_tokens_batch.argtypes = [vp, vp, u32, vp, vp, vp]
+        L.nghttp2_amd_hd_lookup_token.argtypes = [ctypes.c_char_p, sz]
+        L.nghttp2_amd_hd_lookup_token.restype = ctypes.c_int32
+        L.nghttp2_amd_hd_name_hash.argtypes = [ctypes.c_char_p, sz]
+        L.nghttp2_amd_hd_name_hash.restype = ctypes.c_uint32
         _lib = L
     return _lib
+
+
+def lookup_token(name):
+    """Host lookup_token (lib/nghttp2_hd.c:137): -1 or NGHTTP2_TOKEN_*."""
+    name = bytes(name)
+    return lib().nghttp2_amd_hd_lookup_token(name, len(name))
+
+
+def name_hash(name):
+    """Host FNV-1a name hash (lib/nghttp2_hd.c:536-547)."""
+    name = bytes(name)
+    return lib().nghttp2_amd_hd_name_hash(name, len(name))
 
 
 def tables_ref_layout():
@@ -158,6 +175,21 @@ class HuffmanBatchCodec:
             _p(src), _p(src_off), n, _p(enc_len), _stream(stream))
         _check(rv, "encode_count_batch")
         return enc_len[:n]
+
+    def name_tokens(self, names, name_off, token=None, hash=None, stream=None):
+        """lookup_token + name_hash (lib/nghttp2_hd.c:137, :536) for every
+        name of the batch: returns (token int32[n], hash int32[n] holding the
+        uint32 FNV-1a bits)."""
+        torch = self.torch
+        n = name_off.numel() - 1
+        if token is None:
+            token = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        if hash is None:
+            hash = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        rv = self.L.nghttp2_amd_hd_name_tokens_batch(
+            _p(names), _p(name_off), n, _p(token), _p(hash), _stream(stream))
+        _check(rv, "name_tokens_batch")
+        return token[:n], hash[:n]
 
     def emit_strings(self, src, src_off, raw_bytes=None, dst=None, dst_off=None, stream=None):
         """HPACK string literals (emit_string, lib/nghttp2_hd.c:1001-1044) for

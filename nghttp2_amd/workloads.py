@@ -198,3 +198,69 @@ def gen_adversarial(n, seed=SEED[5]):
     allb = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
     out_pool, out_off = _pool_from_lengths(lens, allb)
     return out_pool, out_off, cats
+
+
+# Header names for the token / name-hash batch.
+TOKEN_NAMES = [
+    b":authority", b":method", b":path", b":scheme", b":status", b"accept-charset",
+    b"accept-encoding", b"accept-language", b"accept-ranges", b"accept",
+    b"access-control-allow-origin", b"age", b"allow", b"authorization", b"cache-control",
+    b"content-disposition", b"content-encoding", b"content-language", b"content-length",
+    b"content-location", b"content-range", b"content-type", b"cookie", b"date", b"etag",
+    b"expect", b"expires", b"from", b"host", b"if-match", b"if-modified-since",
+    b"if-none-match", b"if-range", b"if-unmodified-since", b"last-modified", b"link",
+    b"location", b"max-forwards", b"proxy-authenticate", b"proxy-authorization", b"range",
+    b"referer", b"refresh", b"retry-after", b"server", b"set-cookie",
+    b"strict-transport-security", b"transfer-encoding", b"user-agent", b"vary", b"via",
+    b"www-authenticate", b"te", b"connection", b"keep-alive", b"proxy-connection", b"upgrade",
+    b":protocol", b"priority"]
+_NAME_ALPHABET = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_", dtype=np.uint8)
+
+
+def gen_names(n, seed=0x5EED0006, long_frac=0.02):
+    """n header names: ~55% token names, ~12% near misses (one byte changed,
+    upper-cased, cut or extended by a byte), ~30% random x-/custom names of
+    1..40 bytes, ~3% empty; and whole waves (64 aligned names) of long names
+    (100..600 B) with probability long_frac, which exceed the kernel's
+    staging region.  Returns (pool, off)."""
+    rng = np.random.default_rng(seed)
+    kind = rng.choice(4, size=n, p=[0.55, 0.12, 0.30, 0.03])
+    nw = (n + 63) // 64
+    long_wave = rng.random(nw) < long_frac
+    kind[np.repeat(long_wave, 64)[:n]] = 4
+    pick = rng.integers(0, len(TOKEN_NAMES), size=n)
+    lens = np.where(kind == 4, rng.integers(100, 601, size=n), rng.integers(1, 41, size=n))
+    rnd = _NAME_ALPHABET[rng.integers(0, len(_NAME_ALPHABET), size=int(lens.sum()))].tobytes()
+    roff = np.concatenate([[0], np.cumsum(lens)])
+    mut = rng.integers(0, 4, size=n)
+    pos = rng.integers(0, 1 << 30, size=n)
+    bit = rng.integers(0, 7, size=n)
+    out = []
+    for i in range(n):
+        k = kind[i]
+        if k == 0:
+            out.append(TOKEN_NAMES[pick[i]])
+        elif k == 1:
+            b = bytearray(TOKEN_NAMES[pick[i]])
+            m = mut[i]
+            if m == 0:
+                b[pos[i] % len(b)] ^= 1 << int(bit[i])
+            elif m == 1:
+                b = bytearray(bytes(b).upper())
+            elif m == 2:
+                b = b[:-1]
+            else:
+                b.append(rnd[roff[i]])
+            out.append(bytes(b))
+        elif k == 2:
+            out.append(b"x-" + rnd[roff[i]:roff[i + 1]])
+        elif k == 3:
+            out.append(b"")
+        else:
+            out.append(rnd[roff[i]:roff[i + 1]])
+    return names_to_pool(out)
+
+
+def names_to_pool(names):
+    lengths = np.array([len(x) for x in names], dtype=np.int64)
+    return _pool_from_lengths(lengths, np.frombuffer(b"".join(names), dtype=np.uint8))

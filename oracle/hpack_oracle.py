@@ -285,3 +285,37 @@ class Deflater:
                 out += O.encode_length(idx + 1, 6 if mode == _WITH else 4, first)
             out += O.emit_string(v)
         return bytes(out)
+
+
+# ---------------------------------------------------------------------------
+# Header-name tokens and name hash
+# ---------------------------------------------------------------------------
+# lookup_token (lib/nghttp2_hd.c:137-520): a static-table name gives its first
+# static index (the NGHTTP2_TOKEN_* values 0..60, lib/nghttp2_hd.h:57-108);
+# seven more names get 61..67 in enum order (lib/nghttp2_hd.h:109-115).
+_EXTRA_TOKENS = [b"te", b"connection", b"keep-alive", b"proxy-connection", b"upgrade",
+                 b":protocol", b"priority"]
+_TOKENS = dict(_STATIC_TOKEN)
+for _k, _n in enumerate(_EXTRA_TOKENS):
+    _TOKENS[_n] = 61 + _k
+
+
+def lookup_token(name):
+    """lib/nghttp2_hd.c:137-520 -- exact, case-sensitive name match."""
+    return _TOKENS.get(bytes(name), -1)
+
+
+def name_hash(name):
+    """32-bit FNV-1a, lib/nghttp2_hd.c:536-547 (the shift-add form of
+    h *= 16777619)."""
+    h = 2166136261
+    for c in bytes(name):
+        h ^= c
+        h = (h + (h << 1) + (h << 4) + (h << 7) + (h << 8) + (h << 24)) & 0xFFFFFFFF
+    return h
+
+
+def name_tokens(names):
+    """(token[], hash[]) for a list of names: what
+    nghttp2_amd_hd_name_tokens_batch returns."""
+    return [lookup_token(n) for n in names], [name_hash(n) for n in names]

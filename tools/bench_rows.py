@@ -8,6 +8,10 @@
            (host memory), Huffman literals decoded in one GPU batch per
            call; wire MB/s and fields/s, with the split between host passes
            and the GPU round trip.
+  names    nghttp2_amd_hd_name_tokens_batch: lookup_token + name_hash
+           (lib/nghttp2_hd.c:137, :536) over 1M header names, device-resident;
+           algorithmic bytes sum(L) + 12 N (name bytes + offset in, token +
+           hash out) over the kernel time (HIP events on its stream).
 
 Prints one JSON object.  Not the bench.py contract (that is the hot path
 itself); the numbers go to DESIGN.md."""
@@ -50,6 +54,40 @@ def bench_emit(steps=20):
     F = int(do[-1].item())
     return {"strings": len(off) - 1, "raw_bytes": raw, "literal_bytes": F,
             "ms_per_batch": round(t * 1e3, 4), "GBps_raw_plus_out": round((raw + F) / t / 1e9, 1)}
+
+
+def bench_names(steps=50, long_frac=0.02):
+    import torch
+    import nghttp2_amd
+    from nghttp2_amd import workloads as W
+    from oracle import hpack_oracle as H
+    dev = torch.device("cuda:0")
+    pool, off = W.gen_names(1 << 20, long_frac=long_frac)
+    n, raw = len(off) - 1, int(off[-1])
+    codec = nghttp2_amd.HuffmanBatchCodec(dev)
+    names = torch.from_numpy(pool).to(dev)
+    no = torch.from_numpy(off.view(np.int32)).to(dev)
+    tok, h = codec.name_tokens(names, no)
+    torch.cuda.synchronize()
+    k = 20000  # parity on a sample
+    et, eh = H.name_tokens([pool[off[i]:off[i + 1]].tobytes() for i in range(k)])
+    assert np.array_equal(tok[:k].cpu().numpy(), np.array(et, np.int32))
+    assert np.array_equal(h[:k].cpu().numpy().view(np.uint32), np.array(eh, np.uint32))
+    for _ in range(5):
+        codec.name_tokens(names, no, token=tok, hash=h)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(steps):
+        codec.name_tokens(names, no, token=tok, hash=h)
+    e1.record(s)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / steps
+    B = raw + 12 * n
+    return {"names": n, "name_bytes": raw, "us_per_batch": round(t * 1e6, 2),
+            "GBps_algorithmic": round(B / t / 1e9, 1), "hbm_frac": round(B / t / 8.0e12, 4),
+            "Gnames_per_s": round(n / t / 1e9, 3), "long_wave_frac": long_frac}
 
 
 def make_blocks(nconn, per_conn, fields_per_block, seed=7):
@@ -102,4 +140,7 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
 
 
 if __name__ == "__main__":
-    print(json.dumps({"emit": bench_emit(), "inflate": bench_inflate()}, indent=1))
+    rows = sys.argv[1:] or ["emit", "inflate", "names"]
+    fns = {"emit": bench_emit, "inflate": bench_inflate, "names": bench_names,
+           "names_short": lambda: bench_names(long_frac=0.0)}
+    print(json.dumps({r: fns[r]() for r in rows}, indent=1))
