@@ -14,7 +14,8 @@
 // predicated steps); the 64 names of a wave are contiguous in the pool, so
 // their loads share cache lines and HBM sees each byte once.  The 128-slot
 // token table (hd_tokens.h) is staged in LDS once per workgroup (1.6 KB);
-// a hash + length hit is verified with dword compares.  HBM traffic per
+// a hash + length hit is verified with dword compares against the name's
+// bytes still in registers.  HBM traffic per
 // name: its bytes + 4 (offset) in, 8 out -- an HBM-bound byte scan, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,6 +31,20 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 constexpr uint32_t NT_WG = 256;
 
 __constant__ hdtok::Table kTokTable = hdtok::kTable;
+
+// FNV-1a steps over the bytes [a, b) of the 32-byte chunk at cb (branch-free)
+__device__ __forceinline__ uint32_t hash_chunk(uint32_t h, uint4 c0, uint4 c1, uint32_t cb, uint32_t a,
+                                               uint32_t b) {
+  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+  for (uint32_t j = 0; j < 32u; ++j) {
+    const uint32_t p = cb + j;
+    const uint32_t c = (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+    const uint32_t hn = (h ^ c) * hdtok::kFnvPrime;
+    h = (p >= a && p < b) ? hn : h;
+  }
+  return h;
+}
 
 __global__ __launch_bounds__(NT_WG) void k_name_tokens(const uint8_t *__restrict__ names,
                                                        const uint32_t *__restrict__ off, uint32_t n,
@@ -49,57 +64,63 @@ __global__ __launch_bounds__(NT_WG) void k_name_tokens(const uint8_t *__restrict
   if (s >= n) return;
   const uint32_t a = off[s], b = off[s + 1], len = b - a;
   // FNV-1a over 32-byte chunks from the 16-byte aligned base below the name,
-  // the next chunk's loads issued before the current chunk is hashed
+  // the next chunk's loads issued before the current chunk is hashed.  The
+  // first two chunks stay in registers (F) for the token compare: a name of
+  // <= 32 bytes lies within them ((a & 15) + 32 <= 47).
   const uint4 *g = reinterpret_cast<const uint4 *>(names);
   uint32_t h = hdtok::kFnvBasis;
   uint32_t cb = a & ~15u;
-  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
+  uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, n0 = c0, n1 = c0;
   if (a < b) {
     c0 = g[cb >> 4];
     c1 = g[(cb >> 4) + 1u];
   }
+  if (cb + 32u < b) {
+    n0 = g[(cb >> 4) + 2u];
+    n1 = g[(cb >> 4) + 3u];
+  }
+  const uint32_t F[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                          n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+  h = hash_chunk(h, c0, c1, cb, a, b);
+  cb += 32u;
+  c0 = n0;
+  c1 = n1;
   for (; cb < b; cb += 32u) {
-    uint4 n0 = c0, n1 = c1;
     if (cb + 32u < b) {
       n0 = g[(cb >> 4) + 2u];
       n1 = g[(cb >> 4) + 3u];
     }
-    const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-    for (uint32_t j = 0; j < 32u; ++j) {
-      const uint32_t p = cb + j;
-      const uint32_t c = (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
-      const uint32_t hn = (h ^ c) * hdtok::kFnvPrime;
-      h = (p >= a && p < b) ? hn : h;
-    }
+    h = hash_chunk(h, c0, c1, cb, a, b);
     c0 = n0;
     c1 = n1;
   }
-  // token: probe by hash, verify length and bytes (aligned dword loads of
-  // the name, realigned with v_alignbyte; table names are dword aligned and
+  // token: probe by hash, verify length and bytes (the name's dwords
+  // realigned from F with v_alignbyte; table names are dword aligned and
   // zero padded)
   int32_t tok = -1;
   if (len <= 32u) {
+    const uint32_t qw = (a & 15u) >> 2, sh = a & 3u;
+    uint32_t G[9];
+#pragma unroll
+    for (uint32_t j = 0; j < 9u; ++j)
+      G[j] = qw == 0 ? F[j] : qw == 1 ? F[j + 1] : qw == 2 ? F[j + 2] : F[j + 3];
+    uint32_t nm[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i) {
+      uint32_t v = __builtin_amdgcn_alignbyte(G[i + 1], G[i], sh);
+      const uint32_t left = len > 4u * i ? len - 4u * i : 0u;
+      nm[i] = left >= 4u ? v : v & ((1u << (8u * left)) - 1u);
+    }
     for (uint32_t slot = h & (hdtok::kSlots - 1u), k = 0; k < hdtok::kSlots;
          ++k, slot = (slot + 1u) & (hdtok::kSlots - 1u)) {
       const uint32_t m = TM[slot];
       if (m == 0) break;
       if (TH[slot] != h || hdtok::meta_len(m) != len) continue;
-      const uint32_t *gw = reinterpret_cast<const uint32_t *>(names + (a & ~3u));
-      const uint32_t sh = a & 3u, nw = (sh + len + 3u) >> 2;  // aligned words holding the name
-      uint32_t d[9];
-#pragma unroll
-      for (uint32_t i = 0; i < 9u; ++i) d[i] = i < nw ? gw[i] : 0u;
       const lds_u32 *q = TN + (hdtok::meta_off(m) >> 2);
       bool eq = true;
 #pragma unroll
-      for (uint32_t i = 0; i < 8u; ++i) {
-        if (4u * i >= len) break;
-        uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        const uint32_t left = len - 4u * i;
-        if (left < 4u) v &= (1u << (8u * left)) - 1u;
-        eq = eq && v == q[i];
-      }
+      for (uint32_t i = 0; i < 8u; ++i)
+        if (4u * i < len) eq = eq && nm[i] == q[i];
       if (eq) {
         tok = (int32_t)hdtok::meta_token(m);
         break;

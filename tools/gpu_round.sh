@@ -16,7 +16,7 @@ run() {
   echo "== $name rc=$rc"; tail -n 3 "$O/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
 }
-for s in ${STEPS:-pytest smoke bench bench3 host prof pmc}; do
+for s in ${STEPS:-pytest smoke bench bench3 host prof pmc names}; do
   case $s in
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -35,6 +35,9 @@ for s in ${STEPS:-pytest smoke bench bench3 host prof pmc}; do
               run pmc_c${c}_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_c$c/p1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 --config $c
               run pmc_c${c}_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_c$c/p2 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 --config $c
             done ;;
+    names)  rm -rf $O/prof_names
+            run rows_names 300 python tools/bench_rows.py names_short names
+            run prof_names 300 rocprofv3 --kernel-trace --stats -d $O/prof_names -o run --output-format csv -- python3 tools/bench_rows.py names ;;
   esac
 done
 echo "all steps done"
