@@ -88,6 +88,11 @@ void put_int(std::string &out, uint32_t n, uint32_t prefix, uint8_t first) {
 
 struct nghttp2_amd_hd_deflater {
   std::deque<Entry> table;  // front = most recent
+  // name hash -> insertion sequence numbers of the entries with that hash,
+  // oldest first (the reference's hd_map buckets, lib/nghttp2_hd.c:549-611);
+  // the entry with sequence q sits at table[next_seq - 1 - q]
+  std::unordered_map<uint32_t, std::deque<uint64_t>> by_hash;
+  uint64_t next_seq = 0;
   size_t bufsize = 0;
   size_t bufsize_max;                   // ctx.hd_table_bufsize_max
   size_t deflate_max;                   // deflate_hd_table_bufsize_max
@@ -95,20 +100,23 @@ struct nghttp2_amd_hd_deflater {
   bool notify = false;                  // notify_table_size_change
   bool bad = false;
 
-  void shrink() {
-    while (bufsize > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+  void evict_oldest() {
+    const Entry &e = table.back();
+    bufsize -= e.name.size() + e.value.size() + kEntryOverhead;
+    auto it = by_hash.find(e.hash);
+    it->second.pop_front();  // the oldest entry is the oldest of its bucket
+    if (it->second.empty()) by_hash.erase(it);
+    table.pop_back();
   }
-  void add(const uint8_t *n, size_t nl, const uint8_t *v, size_t vl) {
+  void shrink() {
+    while (bufsize > bufsize_max && !table.empty()) evict_oldest();
+  }
+  void add(const uint8_t *n, size_t nl, const uint8_t *v, size_t vl, uint32_t h) {
     const size_t room = nl + vl + kEntryOverhead;
-    while (bufsize + room > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+    while (bufsize + room > bufsize_max && !table.empty()) evict_oldest();
     if (room > bufsize_max) return;
-    table.push_front(Entry{std::string((const char *)n, nl), std::string((const char *)v, vl), name_hash(n, nl)});
+    table.push_front(Entry{std::string((const char *)n, nl), std::string((const char *)v, vl), h});
+    by_hash[h].push_back(next_seq++);
     bufsize += room;
   }
 };
@@ -303,18 +311,22 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
       const bool name_only = mode == NEVER_INDEXING;
       int64_t idx = -1;
       bool exact = false;
-      for (size_t t = 0; t < d->table.size(); ++t) {
-        const Entry &e = d->table[t];
-        if (e.hash != nh || e.name.size() != nv.namelen || memcmp(e.name.data(), nv.name, nv.namelen) != 0)
-          continue;
-        if (idx < 0) {
-          idx = (int64_t)(kStaticLen + t);
-          if (name_only) break;
-        }
-        if (e.value.size() == nv.valuelen && memcmp(e.value.data(), nv.value, nv.valuelen) == 0) {
-          idx = (int64_t)(kStaticLen + t);
-          exact = true;
-          break;
+      auto bucket = d->by_hash.find(nh);
+      if (bucket != d->by_hash.end()) {
+        const std::deque<uint64_t> &seqs = bucket->second;
+        for (size_t r = seqs.size(); r-- > 0;) {  // newest first
+          const size_t t = (size_t)(d->next_seq - 1u - seqs[r]);
+          const Entry &e = d->table[t];
+          if (e.name.size() != nv.namelen || memcmp(e.name.data(), nv.name, nv.namelen) != 0) continue;
+          if (idx < 0) {
+            idx = (int64_t)(kStaticLen + t);
+            if (name_only) break;
+          }
+          if (e.value.size() == nv.valuelen && memcmp(e.value.data(), nv.value, nv.valuelen) == 0) {
+            idx = (int64_t)(kStaticLen + t);
+            exact = true;
+            break;
+          }
         }
       }
       if (!exact && token >= 0 && token <= kLastStaticToken) {  // search_static_table (:1201-1223)
@@ -335,7 +347,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
         P.push_back(pc);
         continue;
       }
-      if (mode == WITH_INDEXING) d->add(nv.name, nv.namelen, nv.value, nv.valuelen);
+      if (mode == WITH_INDEXING) d->add(nv.name, nv.namelen, nv.value, nv.valuelen, nh);
       const uint8_t first = mode == WITH_INDEXING ? 0x40 : mode == WITHOUT_INDEXING ? 0x00 : 0x10;
       if (idx < 0) {  // emit_newname_block (:1104-1128)
         pc.bytes.push_back((char)first);
