@@ -885,22 +885,55 @@ struct NullSink {
   __device__ __forceinline__ void put_nf(uint32_t, uint32_t c8) { n8 += c8; }
   __device__ __forceinline__ void flush() {}
 };
-// Caller slots (any alignment, capacity checked).
-struct CheckedSink {
-  uint8_t *p;
-  uint32_t cap, n;
+// Caller slots (any alignment, capacity checked), dword stores: as
+// UDwordSink, with every store limited to the slot end `lim`; a byte at or
+// past it is not written and marks the overflow.
+struct CheckedDwordSink {
+  uint32_t *p;
+  const uint8_t *lim;
+  uint64_t acc;
+  uint32_t nb, n8, h;
   bool ovf;
-  __device__ __forceinline__ void init(uint8_t *q, uint32_t c) { p = q; cap = c; n = 0; ovf = false; }
-  __device__ __forceinline__ uint32_t count() const { return n; }
-  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
-    if (n < cap) p[n] = (uint8_t)v; else ovf = true;
-    if (c8 > 8u) {
-      if (n + 1 < cap) p[n + 1] = (uint8_t)(v >> 8); else ovf = true;
-    }
-    n += c8 >> 3;
+  __device__ __forceinline__ void init(uint8_t *q, uint32_t cap) {
+    h = (uint32_t)(uintptr_t)q & 3u;
+    p = reinterpret_cast<uint32_t *>(q - h);
+    lim = q + cap;
+    acc = 0;
+    nb = 8u * h;
+    n8 = 0;
+    ovf = false;
   }
-  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) { put(v, c8); }
-  __device__ __forceinline__ void flush() {}
+  __device__ __forceinline__ uint32_t count() const { return n8 >> 3; }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    acc |= (uint64_t)v << nb;
+    nb += c8;
+    n8 += c8;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
+    put_nf(v, c8);
+    flush();
+  }
+  __device__ __forceinline__ void bytes(uint32_t from, uint32_t to) {
+    uint8_t *b = reinterpret_cast<uint8_t *>(p);
+    for (uint32_t x = from; x < to; ++x) {
+      if (b + x < lim) b[x] = (uint8_t)(acc >> (8u * x));
+      else ovf = true;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if (nb >= 32u) {
+      if (h == 0 && reinterpret_cast<const uint8_t *>(p) + 4 <= lim) *p = (uint32_t)acc;
+      else bytes(h, 4u);
+      h = 0;
+      ++p;
+      acc >>= 32;
+      nb -= 32u;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    const uint32_t na = nb >> 3;
+    if (na > h) bytes(h, na);
+  }
 };
 
 // Code longer than the lookup: canonical length by a branch-free search over
@@ -1185,9 +1218,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
           if (slot_ovf) {
             ovf = true;
           } else if (!AUTO) {
-            CheckedSink sk;
+            CheckedDwordSink sk;
             sk.init(dst + o, cap);
             r = decode_item<false>(S.T, ibe, bseg, bseg, bstop, bend, sk, dctr);
+            sk.finish();
             ovf = sk.ovf;
           } else {
             DwordSink sk;
@@ -1259,9 +1293,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
         bool ovf = AUTO && slot_ovf;
         if (e0 != XFAIL && !ovf) {
           if (!AUTO) {
-            CheckedSink sk;
+            CheckedDwordSink sk;
             sk.init(dst + o + min(soff, cap), cap > soff ? cap - soff : 0u);
             r2 = decode_item<false>(S.T, ibe, e0, bseg, bstop, bend, sk, dctr);
+            sk.finish();
             ovf = soff + r2.cnt > cap;  // this piece or an earlier one overflowed
           } else {
             UDwordSink sk;
