@@ -36,12 +36,13 @@ __constant__ hdtok::Table kTokTable = hdtok::kTable;
 __device__ __forceinline__ uint32_t hash_chunk(uint32_t h, uint4 c0, uint4 c1, uint32_t cb, uint32_t a,
                                                uint32_t b) {
   const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  // chunk-relative byte range [lo, hi): each step compares its constant j
+  const int32_t lo = (int32_t)(a - cb), hi = (int32_t)(b - cb);
 #pragma unroll
-  for (uint32_t j = 0; j < 32u; ++j) {
-    const uint32_t p = cb + j;
-    const uint32_t c = (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+  for (int32_t j = 0; j < 32; ++j) {
+    const uint32_t c = (w[j >> 2] >> (8u * (j & 3))) & 0xFFu;
     const uint32_t hn = (h ^ c) * hdtok::kFnvPrime;
-    h = (p >= a && p < b) ? hn : h;
+    h = (j >= lo && j < hi) ? hn : h;
   }
   return h;
 }
