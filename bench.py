@@ -3,21 +3,34 @@
 
 Metric (BASELINE.json): "GB/s HPACK Huffman enc+dec (device-resident,
 batched headers); %HBM roofline".  One step = one batched encode of the
-rank's synthetic header strings (count -> scan -> pack, the emit_string
-pair lib/nghttp2_hd.c:1009/:1037) followed by one batched decode of the
-result (engine-assigned output slots, decode with final=1, exact reference
-status and decode context; hd_inflate_read_huff lib/nghttp2_hd.c:1728-1751).  Inputs are resident in HBM before timing.
+rank's synthetic header strings (count -> pack, the emit_string pair
+lib/nghttp2_hd.c:1009/:1037) followed by one batched decode of the result
+(engine-assigned output slots, decode with final=1, exact reference status
+and decode context; hd_inflate_read_huff lib/nghttp2_hd.c:1728-1751).
+Inputs are resident in HBM before timing.
 
 value = sum over ranks of the algorithmic bytes B = 2R + 2E + 24 per string
  / max-over-ranks wall time of the K timed steps.
-Multi-GPU: independent batches per rank (weak scaling), no collective on the
-data path; the only collectives are the timing barrier and the max.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
+Workloads (BASELINE.json configs; --config):
+  3  (default at 1 GPU) 1M mixed-length values, 16-1024 B Zipf -- the largest
+     single-GPU enc+dec config; the line also carries config 2 as
+     `secondary.config2` (same steps, same accounting)
+  2  1M short pseudo-header strings, 8-64 B
+  4  (default for N > 1) 16M strings from the config-3 generator, one fixed
+     set, byte-balanced contiguous shard per rank (strong scaling), no
+     collective on the data path
+  5  decode-only adversarial batch (1M strings, seed 0x5EED0005): status-
+     checked decode GB/s, B = E + decoded bytes + 12 per string
+Multi-GPU: one process per GPU (torch.distributed.run); the only collectives
+are the timing barrier, the max of the times and the sum of the bytes.
+--backend gloo runs the ranks' collectives on the CPU, so N ranks can share
+one GPU (a test of the multi-rank path on a one-GPU box).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -32,7 +45,9 @@ CONFIG_NAMES = {
     3: "1M mixed-length header values (16-1024 B, Zipf), encode+decode, 1xMI355X",
     4: "16M mixed-length header strings (16-1024 B, Zipf) sharded by bytes across the GPUs "
        "(no collective), encode+decode",
+    5: "decode-only adversarial batch (1M strings: 30-bit codes, EOS, padding cases), 1xMI355X",
 }
+CPU_SAMPLE = 1 << 20  # strings of the cpu_baseline sample (bounded CPU work)
 
 
 def parse():
@@ -40,29 +55,48 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="default: 3 on one GPU, 4 (16M sharded) on more")
     ap.add_argument("--strings", type=int, default=None,
-                    help="strings per GPU (configs 2/3) or in total (config 4)")
+                    help="strings per GPU (configs 2/3/5) or in total (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="config 3: skip the config-2 secondary measurement")
     ap.add_argument("--streams", type=int, default=2,
                     help="pipeline the steps over this many streams (step i on stream i %% S)")
-    ap.add_argument("--graph", action="store_true",
-                    help="time replays of one HIP graph of the step instead of plain stream "
-                         "launches (slower on ROCm 7 here: 0.131 vs 0.124 ms per step)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the cpu_baseline leg (default: every core this job may "
+                         "use: the affinity mask, capped by OMP_NUM_THREADS when set)")
     ap.add_argument("--host-resident", action="store_true",
                     help="also time the pinned-host H2D+D2H round trip")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (auto: nccl = RCCL)")
     return ap.parse_args()
 
 
-def cpu_cores_available():
+def cpu_info():
     try:
-        return len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    usable = aff
+    if omp and omp.isdigit() and int(omp) > 0:
+        usable = min(aff, int(omp))
+    return {"nproc": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
+            "cpu_model": model, "usable": usable}
 
 
-def cpu_baseline(pool, off, threads):
+def cpu_baseline_roundtrip(pool, off, threads):
     """Oracle (port of lib/nghttp2_hd_huffman.c) timed on host cores:
     count+encode then decode(final=1), best of repeats; same B accounting."""
     from oracle import oracle as O
@@ -82,6 +116,44 @@ def cpu_baseline(pool, off, threads):
     return res
 
 
+def cpu_baseline_decode(enc, eoff, threads, gpu_status):
+    """Oracle decode(final=1) of the adversarial batch on host cores, best of
+    repeats; also the per-string status check of the GPU run (the oracle as
+    the checker)."""
+    from oracle import oracle as O
+    res = {}
+    st_ref = None
+    for nth in sorted({1, threads}):
+        best = None
+        for _ in range(4):
+            t0 = time.perf_counter()
+            _, _, st, _, _ = O.decode_batch(enc, eoff, nthreads=nth)
+            t = time.perf_counter() - t0
+            best = t if best is None or t < best else best
+            st_ref = st
+        B = int(eoff[-1]) + int(np.maximum(st_ref, 0).sum()) + 12 * (len(eoff) - 1)
+        res[nth] = (B / best / 1e9, best)
+    return res, bool(np.array_equal(st_ref, gpu_status))
+
+
+def verify_roundtrip(dec, dec_off, pool, off, chunk=1 << 18):
+    """decode(encode(x)) == x for every string, in chunks of strings (the
+    index arrays of a whole 16M-string shard would not fit host memory)."""
+    n = len(off) - 1
+    off64 = off.astype(np.int64)
+    do = dec_off.astype(np.int64)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        ln = off64[a + 1:b + 1] - off64[a:b]
+        tot = int(ln.sum())
+        rel = np.arange(tot) - np.repeat(np.cumsum(ln) - ln, ln)
+        idx = np.repeat(do[a:b], ln) + rel
+        lo, hi = int(idx.min()) if tot else 0, int(idx.max()) + 1 if tot else 0
+        got = dec[lo:hi].cpu().numpy()[idx - lo] if tot else np.zeros(0, np.uint8)
+        if not np.array_equal(got, pool[off64[a]:off64[b]]):
+            raise AssertionError("decode(encode(x)) != x in strings [%d, %d)" % (a, b))
+
+
 def main():
     args = parse()
     import torch
@@ -93,33 +165,99 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg = args.config or (3 if world == 1 else 4)
+    backend = args.backend
+    if backend == "auto":
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend)
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)  # gloo: ranks may share one GPU
+    dev = torch.device("cuda", local % ndev)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
-    seed = W.SEED[args.config] + 7919 * rank  # each rank its own batch (weak scaling)
-    scaling = "weak"
-    if args.config == 2:
-        n = args.strings or (1 << 20)
-        pool, off = W.gen_pseudo_headers(n, seed=seed)
-    elif args.config == 3:
-        n = args.strings or (1 << 20)
-        pool, off = W.gen_mixed_values(n, seed=seed)
-    else:  # one fixed set, byte-balanced contiguous shard per rank (strong)
+    def allreduce(x, op):
+        t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def gen(c, rank_):
+        """(pool, off, scaling, seed text) of configuration c for this rank."""
+        seed = W.SEED[c] + 7919 * rank_  # each rank its own batch (weak scaling)
+        if c == 2:
+            n = args.strings or (1 << 20)
+            pool, off = W.gen_pseudo_headers(n, seed=seed)
+            return pool, off, "weak", "numpy PCG64, seed 0x%X + 7919*rank" % W.SEED[c]
+        if c == 3:
+            n = args.strings or (1 << 20)
+            pool, off = W.gen_mixed_values(n, seed=seed)
+            return pool, off, "weak", "numpy PCG64, seed 0x%X + 7919*rank" % W.SEED[c]
+        # config 4: one fixed set, byte-balanced contiguous shard per rank
         from nghttp2_amd import shard as S
         n_total = args.strings or (1 << 24)
         lengths = W.mixed_lengths(n_total)
         all_off = np.zeros(n_total + 1, dtype=np.int64)
         np.cumsum(lengths, out=all_off[1:])
-        s0, s1 = S.byte_balanced_bounds(all_off, world)[rank]
+        s0, s1 = S.byte_balanced_bounds(all_off, world)[rank_]
         pool, off = W.gen_mixed_range(lengths, s0, s1)
-        n = s1 - s0
-        scaling = "strong"
-    raw_bytes = int(off[-1])
+        return pool, off, "strong", "numpy PCG64, chunk-seeded 0x%X, shard [%d, %d) of %d" % (
+            W.SEED[4], s0, s1, n_total)
 
+    if cfg == 5:
+        out = run_decode_only(args, torch, dist, nghttp2_amd, W, dev, world, rank, allreduce)
+    else:
+        pool, off, scaling, data = gen(cfg, rank)
+        out, ctx = run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce,
+                                 pool, off, cfg, scaling, data)
+        if cfg == 3 and not args.no_secondary:
+            p2, o2, _, _ = gen(2, rank)
+            sec, _ = run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce,
+                                   p2, o2, 2, "weak", "", host_resident=False)
+            out["secondary"] = {"config2": {k: sec[k] for k in ("value", "ms_per_step")}}
+            out["secondary"]["config2"].update(
+                workload=CONFIG_NAMES[2], strings_per_gpu=sec["config"]["strings_per_gpu"],
+                raw_bytes_per_gpu=sec["config"]["raw_bytes_per_gpu"], roofline=sec["roofline"])
+        if rank == 0 and not args.no_cpu_baseline and world == 1:
+            info = cpu_info()
+            threads = args.cpu_threads or info["usable"]
+            ns = min(len(off) - 1, CPU_SAMPLE)
+            sp, so = pool, off[:ns + 1]
+            res = cpu_baseline_roundtrip(sp, so, threads)
+            out["cpu_baseline"] = {
+                "value": round(res[threads][0], 4), "unit": "GB/s", "cores": threads,
+                "kind": "port",
+                "sample": "%d strings (%s) of this workload, oracle/huff_oracle.c (C restatement "
+                          "of lib/nghttp2_hd_huffman.c, gcc -O2), count+encode+decode(final=1), "
+                          "best of 5 after 1 warm-up, %d pthreads; 1 thread: %.4f GB/s"
+                          % (ns, "the whole batch" if ns == len(off) - 1 else "the first",
+                             threads, res[1][0]),
+                "value_1thread": round(res[1][0], 4),
+                "host": {k: info[k] for k in ("cpu_model", "nproc", "affinity",
+                                              "omp_num_threads")}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, off, cfg,
+                  scaling, data, host_resident=None):
+    n = len(off) - 1
+    raw_bytes = int(off[-1])
     src = torch.from_numpy(pool).to(dev)
     src_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    codec0 = nghttp2_amd.HuffmanBatchCodec(dev)
+    # the encoded size, once, to size every pipe's decode pool from the
+    # actual E (not the 30-bit worst case)
+    enc_cap = codec0.encode_bound(raw_bytes, n)
+    probe_enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
+    probe_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    codec0.encode(src, src_off, raw_bytes=raw_bytes, dst=probe_enc, dst_off=probe_off)
+    enc_total = int(probe_off[-1].item()) & 0xFFFFFFFF
+    assert enc_total != 0xFFFFFFFF, "encoded total overflows the uint32 offsets"
+    del probe_enc, probe_off
+    enc_cap = min(enc_cap, enc_total + 4096)  # the kernels never write past dst_cap
+    dec_cap = codec0.decode_bound(enc_total, n)
 
     class Pipe:
         """One stream with its own output buffers and workspace: --streams S
@@ -130,12 +268,10 @@ def main():
         def __init__(self, stream):
             self.codec = nghttp2_amd.HuffmanBatchCodec(dev)
             self.stream = stream
-            self.enc_cap = self.codec.encode_bound(raw_bytes, n)
-            self.enc = torch.empty(self.enc_cap, dtype=torch.uint8, device=dev)
+            self.enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
             self.enc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
             self.dec_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            self.dec = torch.empty(self.codec.decode_bound(self.enc_cap, n), dtype=torch.uint8,
-                                   device=dev)
+            self.dec = torch.empty(dec_cap, dtype=torch.uint8, device=dev)
             self.status = torch.empty(n, dtype=torch.int32, device=dev)
             self.src, self.src_off = src, src_off  # --host-resident: the pipe's own copies
 
@@ -147,23 +283,16 @@ def main():
                               dst_off=self.enc_off, stream=st)
             if evs is not None:
                 evs[1].record(st)
-            self.codec.decode_auto(self.enc, self.enc_off, dst=self.dec, dst_off=self.dec_off,
-                                   status=self.status, stream=st)
+            self.codec.decode_auto(self.enc, self.enc_off, enc_bytes=enc_total, dst=self.dec,
+                                   dst_off=self.dec_off, status=self.status, stream=st)
             if evs is not None:
                 evs[2].record(st)
 
     pipes = [Pipe(torch.cuda.current_stream() if k == 0 else torch.cuda.Stream(device=dev))
              for k in range(max(1, args.streams))]
     P0 = pipes[0]
-    codec, enc, enc_off, dec, dec_off, status = (P0.codec, P0.enc, P0.enc_off, P0.dec,
-                                                 P0.dec_off, P0.status)
-    stream = P0.stream
-
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
-    def step(i=None):
-        P0.run(ev[i] if i is not None else None)
 
     for _ in range(args.warmup):
         for p in pipes:
@@ -173,54 +302,34 @@ def main():
         assert torch.equal(p.status, P0.status) and torch.equal(p.enc_off, P0.enc_off)
 
     # correctness gate on this rank's batch (fails loudly, never measured)
-    st = status.cpu().numpy()
+    st = P0.status.cpu().numpy()
     raw_len = np.diff(off.astype(np.int64))
     assert np.array_equal(st, raw_len), "decode(encode(x)) length mismatch"
-    enc_total = int(enc_off[-1].item())
-    do = dec_off.cpu().numpy().view(np.uint32).astype(np.int64)
-    dh = dec.cpu().numpy()
-    idx = np.repeat(do[:-1], raw_len) + (np.arange(raw_bytes) - np.repeat(off[:-1].astype(np.int64), raw_len))
-    assert np.array_equal(dh[idx], pool[:raw_bytes]), "decode(encode(x)) != x"
+    assert int(P0.enc_off[-1].item()) & 0xFFFFFFFF == enc_total
+    verify_roundtrip(P0.dec, P0.dec_off.cpu().numpy().view(np.uint32), pool, off)
 
     # per-kernel timing (roofline): K plain steps with events on the stream
     for i in range(args.steps):
-        step(i)
+        P0.run(ev[i])
     torch.cuda.synchronize()
 
-    # the timed steps: plain launches on the stream (no events in between),
-    # or (--graph) replays of one HIP graph of the step's launches
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-        graph.replay()
-        torch.cuda.synchronize()
-        assert np.array_equal(status.cpu().numpy(), raw_len), "graph replay mismatch"
-
+    # the timed steps: plain launches on the streams (no events in between)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if graph is not None:
-            graph.replay()
-        else:
-            pipes[i % len(pipes)].run()
+        pipes[i % len(pipes)].run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
 
     B_rank = 2 * raw_bytes + 2 * enc_total + 24 * n
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        b = torch.tensor([float(B_rank)], dtype=torch.float64, device=dev)
-        dist.all_reduce(b, op=dist.ReduceOp.SUM)
-        B_total = float(b.item())
+        import torch.distributed as dist_
+        elapsed = allreduce(elapsed, dist_.ReduceOp.MAX)
+        B_total = allreduce(B_rank, dist_.ReduceOp.SUM)
     else:
         B_total = float(B_rank)
 
@@ -230,24 +339,17 @@ def main():
     value = B_total * args.steps / elapsed / 1e9
 
     # roofline of the dominant kernel: k_decode (one launch per step; the
-    # encode is three launches, k_enc_count + k_scan_tiles + k_encode, whose
-    # sum is reported beside it).  traffic: PMC-measured HBM bytes per launch
-    # of the same kernel on the same config (profiles/, FETCH_SIZE x 2 +
-    # WRITE_SIZE per MI355X_MICROARCH.md), when recorded.
+    # encode is two launches, k_enc_count + k_encode, reported beside it).
+    # traffic: PMC-measured HBM bytes per launch of the same kernel on the
+    # same config (profiles/traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per
+    # MI355X_MICROARCH.md), when recorded for this batch size.
     dec_alg = raw_bytes + enc_total + 12 * n  # reads E + offsets, writes R + status
     enc_alg = raw_bytes + enc_total + 12 * n
     achieved = dec_alg / t_dec / 1e9
-    traffic = None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        tj = json.load(open(tpath)).get("config%d" % args.config, {}).get("k_decode")
-        if tj and tj.get("strings") == n:
-            traffic = tj["hbm_bytes_per_launch"]
     roof = {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic, "alg_bytes_per_launch": dec_alg,
-            "launch_ms": round(t_dec * 1e3, 4), "dec_ms": round(t_dec * 1e3, 4),
-            "enc_ms": round(t_enc * 1e3, 4),
+            "traffic": traffic_for(cfg, n, "k_decode"), "alg_bytes_per_launch": dec_alg,
+            "launch_ms": round(t_dec * 1e3, 4), "enc_ms": round(t_enc * 1e3, 4),
             "enc_achieved": round(enc_alg / t_enc / 1e9, 2)}
 
     out = {"metric": "GB/s HPACK Huffman enc+dec (device-resident, batched headers)",
@@ -255,27 +357,26 @@ def main():
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
            "scaling": scaling, "vs_baseline": None, "dtype": "u8",
-           "data": ("synthetic (numpy PCG64, seed 0x%X + 7919*rank)" % W.SEED[args.config])
-                   if args.config != 4 else "synthetic (numpy PCG64, chunk-seeded 0x%X)" % W.SEED[4],
-           "config": {"workload": CONFIG_NAMES[args.config], "strings_per_gpu": n,
+           "data": "synthetic (%s)" % data,
+           "config": {"workload": CONFIG_NAMES[cfg], "config_id": cfg, "strings_per_gpu": n,
                       "raw_bytes_per_gpu": raw_bytes, "enc_bytes_per_gpu": enc_total,
-                      "E_over_R": round(enc_total / raw_bytes, 4),
+                      "E_over_R": round(enc_total / max(1, raw_bytes), 4),
                       "alg_bytes_per_step_all_gpus": int(B_total),
                       "parallelism": "shard%d (independent batches, no collective)" % world,
                       "streams": len(pipes)},
            "roofline": roof}
 
-    if args.host_resident:
+    if host_resident is None:
+        host_resident = args.host_resident
+    if host_resident:
         # The path as deployed: raw headers start in (pinned) host memory and
         # both results go back to it -- H2D raw pool + offsets, encode,
         # decode, D2H encoded pool + offsets and decoded slots + status, all
-        # async on the pipe's stream.  Steps are pipelined over the same
-        # --streams pipes as `value` (each pipe has its own device input and
-        # pinned outputs), so one step's D2H overlaps the next step's H2D
-        # (the two directions of the link).  Same B accounting as `value`.
+        # async on the pipe's stream, steps pipelined over the --streams
+        # pipes (one step's D2H overlaps the next step's H2D).
         h_src = torch.from_numpy(pool).pin_memory()
         h_off = torch.from_numpy(off.view(np.int32)).pin_memory()
-        dec_used = int(dec_off[-1].item())
+        dec_used = int(P0.dec_off[-1].item()) & 0xFFFFFFFF
         for k, p in enumerate(pipes):
             if k:
                 p.src, p.src_off = torch.empty_like(src), torch.empty_like(src_off)
@@ -310,32 +411,113 @@ def main():
         th = time.perf_counter() - th0
         for p in pipes[:min(len(pipes), args.steps)]:
             assert np.array_equal(p.h_st.numpy(), raw_len)
-            assert np.array_equal(p.h_dec.numpy()[idx], pool[:raw_bytes])
         pcie = (raw_bytes + 4 * (n + 1)) + (enc_total + 4 * (n + 1)) + dec_used + 4 * n
         out["host_resident"] = {
             "value": round(B_rank * args.steps / th / 1e9, 3), "unit": "GB/s",
             "ms_per_step": round(th / args.steps * 1e3, 4),
-            "pcie_bytes_per_step": pcie,
-            "streams": len(pipes),
+            "pcie_bytes_per_step": pcie, "streams": len(pipes),
             "note": "pinned H2D raw+offsets, encode, decode, D2H encoded+offsets, "
                     "decoded slots+status, steps pipelined over the streams; same "
                     "algorithmic-B accounting as value"}
+    return out, None
 
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
-        threads = max(1, min(args.cpu_threads, cpu_cores_available()))
-        res = cpu_baseline(pool, off, threads)
-        out["cpu_baseline"] = {
-            "value": round(res[threads][0], 4), "unit": "GB/s", "cores": threads,
-            "kind": "port",
-            "sample": "the same %d-string batch, oracle/huff_oracle.c (restatement of "
-                      "lib/nghttp2_hd_huffman.c, gcc -O2), count+encode+decode(final=1), "
-                      "best of 5 after 1 warm-up, %d pthreads; 1-thread: %.4f GB/s"
-                      % (n, threads, res[1][0]),
-            "value_1thread": round(res[1][0], 4)}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+
+def traffic_for(cfg, n, kernel):
+    tpath = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    tj = json.load(open(tpath)).get("config%d" % cfg, {}).get(kernel)
+    if tj and tj.get("strings") == n:
+        return tj["hbm_bytes_per_launch"]
+    return None
+
+
+def run_decode_only(args, torch, dist, nghttp2_amd, W, dev, world, rank, allreduce):
+    """Config 5: decode(final=1) of the adversarial batch, engine slots; the
+    per-string status is checked against the generator's construction (valid
+    categories decode to their symbol count, embedded EOS and over-long
+    padding fail) and, in the cpu_baseline leg, against the oracle."""
+    n = args.strings or (1 << 20)
+    pool, off, cats, nsym = W.gen_adversarial(n, seed=W.SEED[5] + 7919 * rank, return_nsym=True)
+    E = int(off[-1])
+    src = torch.from_numpy(pool).to(dev)
+    so = torch.from_numpy(off.view(np.int32)).to(dev)
+    codec = nghttp2_amd.HuffmanBatchCodec(dev)
+    cap = codec.decode_bound(E, n)
+    pipes = []
+    for k in range(max(1, args.streams)):
+        s = torch.cuda.current_stream() if k == 0 else torch.cuda.Stream(device=dev)
+        pipes.append((s, torch.empty(cap, dtype=torch.uint8, device=dev),
+                      torch.empty(n + 1, dtype=torch.int32, device=dev),
+                      torch.empty(n, dtype=torch.int32, device=dev)))
+
+    def run(p):
+        s, dst, doff, st = p
+        codec.decode_auto(src, so, enc_bytes=E, dst=dst, dst_off=doff, status=st, stream=s)
+
+    for _ in range(args.warmup):
+        for p in pipes:
+            run(p)
+    torch.cuda.synchronize()
+    st = pipes[0][3].cpu().numpy()
+    valid = np.isin(cats, [0, 5, 6])
+    assert np.array_equal(st[valid], nsym[valid]), "valid adversarial strings mis-decoded"
+    assert (st[np.isin(cats, [1, 2])] == -523).all(), "EOS / long padding not rejected"
+    written = int(np.maximum(st, 0).sum())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    s0 = pipes[0][0]
+    for i in range(args.steps):
+        ev[i][0].record(s0)
+        run(pipes[0])
+        ev[i][1].record(s0)
+    torch.cuda.synchronize()
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(pipes[i % len(pipes)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    B_rank = E + written + 12 * n
+    if world > 1:
+        elapsed = allreduce(elapsed, dist.ReduceOp.MAX)
+        B_total = allreduce(B_rank, dist.ReduceOp.SUM)
+    else:
+        B_total = float(B_rank)
+    t_dec = np.mean([a.elapsed_time(b) for a, b in ev]) * 1e-3
+    achieved = B_rank / t_dec / 1e9
+    out = {"metric": "GB/s HPACK Huffman decode (device-resident, adversarial batch)",
+           "value": round(B_total * args.steps / elapsed / 1e9, 3), "unit": "GB/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (gen_adversarial, seed 0x%X + 7919*rank)" % W.SEED[5],
+           "config": {"workload": CONFIG_NAMES[5], "config_id": 5, "strings_per_gpu": n,
+                      "enc_bytes_per_gpu": E, "decoded_bytes_per_gpu": written,
+                      "failing_strings": int((st < 0).sum()),
+                      "parallelism": "shard%d (independent batches, no collective)" % world,
+                      "streams": len(pipes)},
+           "roofline": {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5),
+                        "traffic": traffic_for(5, n, "k_decode"),
+                        "alg_bytes_per_launch": B_rank, "launch_ms": round(t_dec * 1e3, 4)}}
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        info = cpu_info()
+        threads = args.cpu_threads or info["usable"]
+        res, same = cpu_baseline_decode(pool[:E + 16], off, threads, st)
+        assert same, "GPU status differs from the oracle on the adversarial batch"
+        out["cpu_baseline"] = {
+            "value": round(res[threads][0], 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "the whole %d-string batch, oracle/huff_oracle.c decode(final=1), best of "
+                      "4, %d pthreads; 1 thread: %.4f GB/s; per-string status equal to the "
+                      "GPU's" % (n, threads, res[1][0]),
+            "value_1thread": round(res[1][0], 4),
+            "host": {k: info[k] for k in ("cpu_model", "nproc", "affinity", "omp_num_threads")}}
+    return out
 
 
 if __name__ == "__main__":

@@ -49,6 +49,12 @@ extern "C" {
 #define NGHTTP2_AMD_ERR_FATAL (-900)            /* nghttp2.h:451 (HIP error) */
 #define NGHTTP2_AMD_ERR_NOMEM (-901)            /* nghttp2.h:455 */
 
+/* dst_off[n] after nghttp2_amd_hd_huff_encode_batch when the batch's encoded
+ * total does not fit min(dst_cap, 0xFFFFFFFE): offsets are uint32, so such a
+ * batch must be split (no offset of it is valid, no byte was written past
+ * dst_cap). */
+#define NGHTTP2_AMD_OFF_OVERFLOW 0xFFFFFFFFu
+
 /* Decode-context flag bits (lib/nghttp2_hd_huffman.h:35-37). */
 #define NGHTTP2_AMD_HUFF_ACCEPTED 0x01u
 #define NGHTTP2_AMD_HUFF_SYM 0x02u
@@ -107,10 +113,12 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw
  *                       nghttp2_amd_hd_huff_encode_workspace_size(raw, n) is faster
  *
  * Output bytes equal lib/nghttp2_hd_huffman.c's, including the EOS-prefix
- * (all ones) padding of the last byte.  dst_cap must be >=
- * nghttp2_amd_hd_huff_encode_bound(src_off[n]-src_off[0], n); a smaller
- * capacity returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT (the kernels never
- * write past dst_cap).
+ * (all ones) padding of the last byte.  Size dst_cap by
+ * nghttp2_amd_hd_huff_encode_bound(src_off[n]-src_off[0], n); the kernels
+ * never write past dst_cap.  Offsets are uint32: when the encoded total
+ * would pass min(dst_cap, 0xFFFFFFFE) the batch writes no bytes and
+ * dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW (check it after the stream
+ * synchronises; split the batch).
  */
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst, size_t dst_cap,
@@ -197,7 +205,10 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, cons
  * -- the reference's allocation -- so no string can overflow; bytes of a
  * slot past its decoded length are unspecified.  dst (16-byte aligned) must
  * hold nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes; strings whose slot
- * would end past dst_cap get -502 and write nothing.
+ * would end past dst_cap get -502, write nothing, and their dst_off entries
+ * saturate at dst_cap.  Slots are uint32 offsets: dst_cap > 0xFFFFFFFF
+ * returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT (split a batch whose
+ * decode_bound passes 4 GiB).
  */
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint8_t *dst, size_t dst_cap,

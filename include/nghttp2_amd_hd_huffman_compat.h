@@ -71,7 +71,10 @@ typedef struct {
 } nghttp2_hd_huff_decode_context;
 #endif /* NGHTTP2_AMD_HAVE_NGHTTP2_TYPES */
 
-/* lib/nghttp2_hd.h:394 -- encoded length incl. EOS-prefix padding */
+/* lib/nghttp2_hd.h:394 -- encoded length incl. EOS-prefix padding.  If the
+ * engine fails (no device, no memory) it returns len, so emit_string
+ * (lib/nghttp2_hd.c:1011) takes the raw form rather than framing a
+ * zero-length Huffman literal. */
 NGHTTP2_AMD_EXTERN size_t nghttp2_hd_huff_encode_count(const uint8_t *src, size_t len);
 
 /* lib/nghttp2_hd.h:408-409 -- appends the encoding of src to bufs; 0 or

@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <deque>
 #include <unordered_map>
 #include <mutex>
@@ -141,6 +142,16 @@ bool hip_ok(hipError_t e, const char *what) {
   fprintf(stderr, "nghttp2_amd_hd (deflate): %s: %s\n", what, hipGetErrorString(e));
   return false;
 }
+// Fault injection for the error paths (tests only, like the reference's
+// failmalloc suite, tests/failmalloc_test.c): the next n GPU stages of
+// nghttp2_amd_hd_deflate_blocks fail before any HIP call.
+std::atomic<int> g_fail_gpu{0};
+bool fault_inject_gpu() {
+  int k = g_fail_gpu.load();
+  while (k > 0)
+    if (g_fail_gpu.compare_exchange_weak(k, k - 1)) return true;
+  return false;
+}
 bool grow_host(void **p, size_t *cap, size_t need) {
   if (need <= *cap) return true;
   if (*p) (void)hipHostFree(*p);
@@ -170,6 +181,8 @@ struct Piece {
 }  // namespace
 
 extern "C" {
+
+NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__test_fail_deflate_gpu(int n) { g_fail_gpu.store(n); }
 
 int nghttp2_amd_hd_deflate_new(nghttp2_amd_hd_deflater **deflater_ptr,
                                size_t max_deflate_dynamic_table_size) {
@@ -360,15 +373,17 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     }
   };
   {
-    std::unordered_map<nghttp2_amd_hd_deflater *, std::vector<uint32_t>> groups;
-    std::vector<nghttp2_amd_hd_deflater *> conns;
+    // the batch's lists per connection, in batch order; the parallel region
+    // only reads `lists` (a vector indexed by connection number)
+    std::unordered_map<nghttp2_amd_hd_deflater *, uint32_t> conn_of;
+    std::vector<std::vector<uint32_t>> lists;
     for (uint32_t i = 0; i < nblocks; ++i) {
-      auto &g = groups[deflaters[i]];
-      if (g.empty()) conns.push_back(deflaters[i]);
-      g.push_back(i);
+      auto it = conn_of.emplace(deflaters[i], (uint32_t)lists.size()).first;
+      if (it->second == lists.size()) lists.emplace_back();
+      lists[it->second].push_back(i);
     }
-    parallel_for(conns.size(), 1, [&](size_t c) {
-      for (uint32_t i : groups[conns[c]]) deflate_list(i);
+    parallel_for(lists.size(), 1, [&](size_t c) {
+      for (uint32_t i : lists[c]) deflate_list(i);
     });
   }
   // literal numbering: block i's literals are litbase[i] + j
@@ -382,6 +397,21 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   }
 
   ph.mark("tables");
+  // Pass 1 has changed the deflaters (entries inserted, size updates
+  // consumed).  From here on a failure leaves the encoder tables ahead of
+  // what the peer will receive, so every deflater of the batch turns bad and
+  // every block not failed already reports the error, as
+  // nghttp2_hd_deflate_hd_bufs sets ctx.bad on each failure path
+  // (lib/nghttp2_hd.c:1509-1516).
+  auto fail_batch = [&](int rv) {
+    for (uint32_t i = 0; i < nblocks; ++i) {
+      deflaters[i]->bad = true;
+      if (block_status[i] >= 0) block_status[i] = rv;
+      out_off[i + 1] = 0;
+    }
+    out_off[0] = 0;
+    return rv;
+  };
   // ---- GPU: frame every literal of the batch (emit_string)
   const uint32_t nl = litbase[nblocks];
   std::lock_guard<std::mutex> guard(engine().mu);
@@ -391,7 +421,9 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   if (nl) {
     hipStream_t st = (hipStream_t)stream;
     const uint64_t raw = rawbase[nblocks];
-    if (raw > UINT32_MAX) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
+    // uint32 offsets: the framed literals (raw + <= 6 prefix bytes each)
+    if (nghttp2_amd_hd_emit_strings_bound(raw, nl) > UINT32_MAX)
+      return fail_batch(NGHTTP2_AMD_ERR_INVALID_ARGUMENT);
     const size_t in_bytes = ((size_t)raw + 15u) / 16u * 16u + 16u;
     const size_t out_bytes = nghttp2_amd_hd_emit_strings_bound(raw, nl);
     const size_t ws = nghttp2_amd_hd_emit_strings_workspace_size(raw, nl);
@@ -402,7 +434,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
         !grow_dev((void **)&E.d_out, &E.dout_cap, out_bytes) ||
         !grow_dev((void **)&E.d_ws, &E.dws_cap, ws) ||
         !grow_dev((void **)&E.d_off, &E.doff_cap, 2u * ((size_t)nl + 1u) * sizeof(uint32_t)))
-      return NGHTTP2_AMD_ERR_NOMEM;
+      return fail_batch(NGHTTP2_AMD_ERR_NOMEM);
     // the literal pool and its offsets, block by block
     parallel_for(nblocks, 256, [&](size_t i) {
       uint32_t o = (uint32_t)rawbase[i];
@@ -417,18 +449,19 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     memset(E.h_in + raw, 0, in_bytes - raw);
     uint32_t *d_fo = E.d_off + (nl + 1);
     uint32_t *h_fo = E.h_off + (nl + 1);
-    if (!hip_ok(hipMemcpyAsync(E.d_in, E.h_in, in_bytes, hipMemcpyHostToDevice, st), "H2D") ||
+    if (fault_inject_gpu() ||
+        !hip_ok(hipMemcpyAsync(E.d_in, E.h_in, in_bytes, hipMemcpyHostToDevice, st), "H2D") ||
         !hip_ok(hipMemcpyAsync(E.d_off, E.h_off, (nl + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st), "H2D"))
-      return NGHTTP2_AMD_ERR_FATAL;
+      return fail_batch(NGHTTP2_AMD_ERR_FATAL);
     int rv = nghttp2_amd_hd_emit_strings_batch(E.d_in, E.d_off, nl, raw, E.d_out, out_bytes, d_fo,
                                                E.d_ws, ws, stream);
-    if (rv) return rv;
+    if (rv) return fail_batch(rv);
     if (!hip_ok(hipMemcpyAsync(h_fo, d_fo, (nl + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "D2H") ||
         !hip_ok(hipStreamSynchronize(st), "sync"))
-      return NGHTTP2_AMD_ERR_FATAL;
+      return fail_batch(NGHTTP2_AMD_ERR_FATAL);
     if (!hip_ok(hipMemcpyAsync(E.h_out, E.d_out, h_fo[nl], hipMemcpyDeviceToHost, st), "D2H") ||
         !hip_ok(hipStreamSynchronize(st), "sync"))
-      return NGHTTP2_AMD_ERR_FATAL;
+      return fail_batch(NGHTTP2_AMD_ERR_FATAL);
     fr = E.h_out;
     froff = h_fo;
   }
@@ -457,7 +490,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
       // an earlier block of this deflater ran out of room in this call:
       // later ones fail as nghttp2_hd_deflate_hd_bufs does (:1475-1477)
       block_status[i] = NGHTTP2_AMD_ERR_HEADER_COMP;
-    } else if (block_status[i] == 0 && o + need[i] > out_cap) {
+    } else if (block_status[i] == 0 && (o + need[i] > out_cap || o + need[i] > UINT32_MAX)) {
       // INSUFF_BUFSIZE in nghttp2_hd_deflate_hd2 (:1546-1547); the deflater turns bad
       block_status[i] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
       deflaters[i]->bad = true;

@@ -489,10 +489,11 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
   uint4 wn = make_uint4(0, 0, 0, 0);  // the next round's chunk (prefetched)
   if ((A >> 4) + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + (((A >> 4) + lane) << 4));
   // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
-  // strings, L2-resident), summed with independent loads in flight
-  uint32_t pre = 0;
+  // strings, L2-resident), summed with independent loads in flight, in 64
+  // bits (a batch's encoded total may pass the uint32 offset range)
+  uint64_t pre = 0;
   {
-    uint32_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t t = threadIdx.x;
     for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
 #pragma unroll
@@ -502,8 +503,24 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
 #pragma unroll
     for (int k = 0; k < 8; ++k) pre += p8[k];
   }
-  uint32_t tot, ptot;
-  const uint32_t o_me = block_excl_scan_sum<WG>(E_me, pre, red, &tot, &ptot) + ptot;  // (barriers)
+  uint32_t tot, ptot_lo, ptot_hi;
+  // the 64-bit prefix as two 32-bit sums: 256 parts of 23 bits fit 31 bits
+  const uint32_t loc = block_excl_scan_sum<WG>(E_me, (uint32_t)(pre & 0x7FFFFFu), red, &tot,
+                                               &ptot_lo);  // (barriers)
+  {
+    uint32_t dummy;
+    block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
+  }
+  const uint64_t ptot = ((uint64_t)ptot_hi << 23) + ptot_lo;
+  // uint32 offsets: a tile whose strings would end past the limit writes no
+  // bytes, saturated offsets and the overflow mark in dst_off[n]
+  const uint64_t limit = dst_cap < 0xFFFFFFFEull ? dst_cap : 0xFFFFFFFEull;
+  if (ptot + tot > limit) {
+    if (s_me < n) dst_off[s_me] = (uint32_t)min(ptot + loc, limit);
+    if (s_me == n - 1u) dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW;
+    return;
+  }
+  const uint32_t o_me = (uint32_t)ptot + loc;
   if (s_me < n) dst_off[s_me] = o_me;
   if (s_me == n - 1u) dst_off[n] = o_me + E_me;
   o_sh[threadIdx.x] = o_me;
@@ -1135,9 +1152,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
     const bool sl = lane < nstr;
     const uint32_t a_l = sl ? off[t0 + lane] : 0u;
     const uint32_t b_l = sl ? off[t0 + lane + 1] : 0u;
-    if (AUTO && sl) {
-      dst_off[t0 + lane] = (uint32_t)auto_slot(a_l - off0, t0 + lane);
-      if (t0 + lane == n - 1) dst_off[n] = (uint32_t)auto_slot(b_l - off0, n);
+    if (AUTO && sl) {  // saturated at dst_cap (< 2^32, checked by the host)
+      dst_off[t0 + lane] = (uint32_t)min(auto_slot(a_l - off0, t0 + lane), dst_cap);
+      if (t0 + lane == n - 1) dst_off[n] = (uint32_t)min(auto_slot(b_l - off0, n), dst_cap);
     }
     const uint32_t m_l = sl ? (b_l - a_l > PIECE_BYTES ? (b_l - a_l + PIECE_BYTES - 1u) / PIECE_BYTES : 1u) : 0u;
     const uint32_t P_l = wave_incl_scan(m_l);       // items through string l
@@ -1668,6 +1685,7 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 slots
   hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>, DEC_NT, TASK_STR * DEC_WAVES>(n)), dim3(DEC_NT), 0, st, src, src_off,
                      n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());

@@ -97,15 +97,20 @@ bool upload(Single &s, const uint8_t *src, size_t len) {
 
 extern "C" {
 
+// The reference's count cannot fail.  When the engine does (no device, out
+// of memory, a string past the uint32 range) the count returned is `len`:
+// emit_string then takes the raw form (it uses Huffman only when
+// enclen < len, lib/nghttp2_hd.c:1011), a valid literal, never a zero
+// length prefix followed by Huffman bytes.
 size_t nghttp2_hd_huff_encode_count(const uint8_t *src, size_t len) {
   Single &s = eng();
   std::lock_guard<std::mutex> g(s.mu);
-  if (len > 0xFFFFFFF0u || !reserve(s, len, 64) || !upload(s, src, len)) return 0;
+  if (len > 0xFFFFFFF0u || !reserve(s, len, 64) || !upload(s, src, len)) return len;
   uint32_t e = 0;
   if (nghttp2_amd_hd_huff_encode_count_batch(s.d_in, s.d_meta, 1, s.d_meta + 4, s.st) != 0 ||
       !hip_ok(hipMemcpyAsync(&e, s.d_meta + 4, 4, hipMemcpyDeviceToHost, s.st)) ||
       !hip_ok(hipStreamSynchronize(s.st)))
-    return 0;
+    return len;
   return e;
 }
 

@@ -22,6 +22,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cassert>
 #include <deque>
 #include <unordered_map>
 #include <mutex>
@@ -475,7 +477,18 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       }
     }
   }
-  for (uint32_t k = 0; k < nh; ++k) hoff[k + 1] = hoff[k] + huff[k]->len;
+  {
+    // uint32 offsets into the batch's literal pool (and uint32 decode slots):
+    // a batch past them is refused before any connection state changes
+    uint64_t tot = 0;
+    for (uint32_t k = 0; k < nh; ++k) {
+      tot += huff[k]->len;
+      if (tot > UINT32_MAX) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+      hoff[k + 1] = (uint32_t)tot;
+    }
+    if (nh && nghttp2_amd_hd_huff_decode_bound(tot, nh) > UINT32_MAX)
+      return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  }
 
   ph.mark("parse");
   // ---- GPU: every Huffman literal of the batch in one decode
@@ -525,21 +538,55 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   // ---- pass 2: each connection's blocks in batch order against its table
   // (one task per connection), fields into per-block buffers
   const LitSrc ls{dec, slot, hst};
-  std::unordered_map<nghttp2_amd_hd_inflater *, std::vector<uint32_t>> groups;
+  // the batch's blocks per connection, in batch order; the parallel region
+  // only reads `lists` (a vector indexed by connection number)
+  std::unordered_map<nghttp2_amd_hd_inflater *, uint32_t> conn_of;
   std::vector<nghttp2_amd_hd_inflater *> conns;
+  std::vector<std::vector<uint32_t>> lists;
   for (uint32_t i = 0; i < nblocks; ++i) {
-    auto &g = groups[inflaters[i]];
-    if (g.empty()) conns.push_back(inflaters[i]);
-    g.push_back(i);
+    auto it = conn_of.emplace(inflaters[i], (uint32_t)conns.size()).first;
+    if (it->second == conns.size()) {
+      conns.push_back(inflaters[i]);
+      lists.emplace_back();
+    }
+    lists[it->second].push_back(i);
   }
-  // snapshots: a batch that outgrows the caller's buffers is cut at the first
-  // block that does not fit, and the tables replayed up to there
+  // A batch that outgrows the caller's buffers is cut at the first block
+  // that does not fit, and the tables replayed up to there, from snapshots.
+  // The snapshots (a copy of every table) are taken only when an upper bound
+  // of the output can pass the caps: a field per representation, its name
+  // and value NUL-terminated; a literal's bytes (decoded length for a
+  // Huffman one); a table reference at most the larger of the longest static
+  // entry and the connection's table limit.
+  bool may_cut = false;
+  {
+    std::vector<size_t> ref_max(conns.size());
+    for (size_t c = 0; c < conns.size(); ++c)
+      ref_max[c] = std::max<size_t>({64u, conns[c]->settings_max, conns[c]->bufsize_max});
+    uint64_t nv_bound = 0, ar_bound = 0;
+    auto lit_len = [&](const Lit &l) -> uint64_t {
+      if (l.huff < 0) return l.len;
+      return hst[l.huff] >= 0 ? (uint64_t)hst[l.huff] : (uint64_t)l.len * 8u / 5u + 1u;
+    };
+    for (uint32_t i = 0; i < nblocks && !may_cut; ++i) {
+      const uint64_t rm = ref_max[conn_of[inflaters[i]]];
+      for (const Op &op : bl[i].ops) {
+        if (op.kind == Op::SIZE) continue;
+        ++nv_bound;
+        if (op.kind == Op::INDEXED) ar_bound += rm + 2u;
+        else ar_bound += (op.new_name ? lit_len(op.name) : rm) + lit_len(op.val) + 2u;
+      }
+      may_cut = nv_bound > nva_cap || ar_bound > arena_cap;
+    }
+  }
   std::vector<nghttp2_amd_hd_inflater> snap;
-  snap.reserve(conns.size());
-  for (auto *c : conns) snap.push_back(*c);
+  if (may_cut) {
+    snap.reserve(conns.size());
+    for (auto *c : conns) snap.push_back(*c);
+  }
   std::vector<BlockOut> outs(nblocks);
   parallel_for(conns.size(), 1, [&](size_t c) {
-    for (uint32_t i : groups[conns[c]]) replay_block(conns[c], bl[i], ls, outs[i]);
+    for (uint32_t i : lists[c]) replay_block(conns[c], bl[i], ls, outs[i]);
   });
 
   ph.mark("replay");
@@ -555,6 +602,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     }
   }
   if (cut < nblocks) {  // restore, then re-apply the blocks before the cut
+    assert(may_cut);  // the bound covers every output that fits no cap
     for (size_t c = 0; c < conns.size(); ++c) *conns[c] = std::move(snap[c]);
     BlockOut scratch;
     for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, scratch);

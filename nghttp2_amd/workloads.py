@@ -154,12 +154,16 @@ def pack_symbols(sym_pool, sym_off, pad_bits_value=None):
     return pool, enc_off.astype(np.uint32), pad
 
 
-def gen_adversarial(n, seed=SEED[5]):
+def gen_adversarial(n, seed=SEED[5], return_nsym=False):
     """Config 5: decode-only adversarial batch.  Category per string (id in
     cats[i]): 0 valid 30-bit symbols (10, 13, 22) + 28-bit control bytes;
     1 embedded EOS; 2 padding of 8-15 ones; 3 zero-bit padding; 4 truncated
     long code; 5 valid text with 0-7 bit all-ones padding; 6 empty;
-    7 random bytes.  Returns (enc_pool, enc_off, cats)."""
+    7 random bytes.  Returns (enc_pool, enc_off, cats[, nsym]); nsym[i] is
+    the number of symbols packed into string i before any corruption (the
+    decoded length of a valid string).  Vectorised; the random draws keep
+    the order of the original per-string generator, so a seed gives the
+    same batch."""
     rng = np.random.Generator(np.random.PCG64(seed))
     cats = rng.integers(0, 8, size=n)
     nsym = rng.integers(1, 24, size=n)
@@ -181,22 +185,36 @@ def gen_adversarial(n, seed=SEED[5]):
     syms[eos_pos[m]] = 256
     pool, enc_off, pad = pack_symbols(syms, sym_off)
     enc_off = enc_off.astype(np.int64)
-    chunks = []
-    for i in range(n):
-        s = pool[enc_off[i]:enc_off[i + 1]].copy()
-        c = cats[i]
-        if c == 2 and len(s):
-            s = np.append(s, np.uint8(0xFF))  # pad becomes 8..15 ones
-        elif c == 3 and len(s) and pad[i] > 0:
-            s[-1] &= np.uint8((0xFF << pad[i]) & 0xFF)  # zero-bit padding
-        elif c == 4 and len(s) > 1:
-            s = s[:-1]  # cut inside the trailing 28/30-bit code
-        elif c == 7:
-            s = rng.integers(0, 256, size=int(rng.integers(1, 40)), dtype=np.uint8)
-        chunks.append(s)
-    lens = np.array([len(s) for s in chunks], dtype=np.int64)
-    allb = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
-    out_pool, out_off = _pool_from_lengths(lens, allb)
+    L = np.diff(enc_off)
+    new_len = L.copy()
+    c2 = (cats == 2) & (L > 0)  # one more 0xFF byte: the pad becomes 8..15 ones
+    c3 = (cats == 3) & (L > 0) & (pad > 0)  # zero-bit padding
+    c4 = (cats == 4) & (L > 1)  # cut inside the trailing 28/30-bit code
+    r7 = np.nonzero(cats == 7)[0]  # random bytes
+    new_len[c2] += 1
+    new_len[c4] -= 1
+    rand7 = []
+    for _ in r7:
+        k = int(rng.integers(1, 40))
+        rand7.append(rng.integers(0, 256, size=k, dtype=np.uint8))
+    new_len[r7] = [len(x) for x in rand7]
+    out_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(new_len, out=out_off[1:])
+    allb = np.zeros(int(out_off[-1]), dtype=np.uint8)
+
+    def spans(starts, lens):  # concatenated index ranges [starts[i], starts[i] + lens[i])
+        tot = int(lens.sum())
+        return np.repeat(starts, lens) + (np.arange(tot) - np.repeat(np.cumsum(lens) - lens, lens))
+
+    cl = np.where(cats != 7, np.minimum(L, new_len), 0)
+    allb[spans(out_off[:-1], cl)] = pool[spans(enc_off[:-1], cl)]
+    allb[out_off[1:][c2] - 1] = 0xFF
+    allb[out_off[1:][c3] - 1] &= ((0xFF << pad[c3]) & 0xFF).astype(np.uint8)
+    if len(r7):
+        allb[spans(out_off[r7], new_len[r7])] = np.concatenate(rand7)
+    out_pool, out_off = _pool_from_lengths(new_len, allb)
+    if return_nsym:
+        return out_pool, out_off, cats, nsym
     return out_pool, out_off, cats
 
 

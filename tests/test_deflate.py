@@ -187,3 +187,29 @@ def test_deflate_buffer_error_is_sticky():
     assert oo[2] == 0
     st2, w2 = nghttp2_amd.deflate_blocks([d], [[(b":method", b"GET")]])
     assert st2[0] == hd.NGHTTP2_ERR_HEADER_COMP and w2[0] == b""
+
+
+def test_deflate_gpu_stage_failure_turns_deflaters_bad_cpu():
+    """A failure after pass 1 (which has already changed the tables) marks
+    every deflater of the batch bad and reports the error on every block, as
+    nghttp2_hd_deflate_hd_bufs sets ctx.bad on each failure path
+    (lib/nghttp2_hd.c:1509-1516).  The fault hook fails the GPU stage before
+    any HIP call, so this runs without a GPU."""
+    import ctypes
+    import nghttp2_amd
+    from nghttp2_amd import hd
+    L = hd._deflate_lib()
+    L.nghttp2_amd_hd__test_fail_deflate_gpu.argtypes = [ctypes.c_int]
+    L.nghttp2_amd_hd__test_fail_deflate_gpu.restype = None
+    d1, d2 = nghttp2_amd.HpackDeflater(), nghttp2_amd.HpackDeflater()
+    lists = [[(b"x-custom", b"value-one")], [(b":method", b"GET"), (b"x-other", b"two")]]
+    L.nghttp2_amd_hd__test_fail_deflate_gpu(1)
+    try:
+        with pytest.raises(RuntimeError):
+            nghttp2_amd.deflate_blocks([d1, d2], lists)
+    finally:
+        L.nghttp2_amd_hd__test_fail_deflate_gpu(0)
+    # both deflaters are bad: even an indexed-only list (no GPU work) fails
+    for d in (d1, d2):
+        st, w = nghttp2_amd.deflate_blocks([d], [[(b":method", b"GET")]])
+        assert st[0] == hd.NGHTTP2_ERR_HEADER_COMP and w[0] == b""

@@ -1,0 +1,264 @@
+"""Large batches on the GPU: BASELINE.json config 4 (16M strings sharded over
+8 GPUs) and config 5 (1M adversarial strings, decode only) at full size, the
+uint32 offset limits, the multi-rank bench path, and the link-level drop-in's
+per-call latency.
+
+- config 4, rank 0's byte-balanced shard of the 16M set (~2M strings,
+  ~314 MB): encode + decode_auto bit-exact against the oracle (16 threads);
+- config 4, the whole 16M set on one GPU (~2.5 GB raw): size-independent
+  properties, decode(encode(x)) == x and status == length for every string;
+- config 5: status, final {fstate, flags} and every written byte (the
+  partial output of failing strings included) against the oracle;
+- an encoded total past 4 GiB is refused (NGHTTP2_AMD_OFF_OVERFLOW), a
+  decode pool past 4 GiB is refused (INVALID_ARGUMENT);
+- bench.py as 2 ranks (gloo) sharing the one GPU: the N > 1 code path.
+"""
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def to_dev(a, dev):
+    import torch
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).to(dev)
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def test_config4_rank0_shard_bit_exact(codec, dev):
+    import torch
+    from nghttp2_amd import shard as S
+    from nghttp2_amd import workloads as W
+    lengths = W.mixed_lengths(1 << 24)
+    all_off = np.zeros(len(lengths) + 1, dtype=np.int64)
+    np.cumsum(lengths, out=all_off[1:])
+    s0, s1 = S.byte_balanced_bounds(all_off, 8)[0]
+    pool, off = W.gen_mixed_range(lengths, s0, s1)
+    n, raw = s1 - s0, int(off[-1])
+    assert n > 1_900_000 and raw > 300_000_000
+    src, so = to_dev(pool, dev), to_dev(off, dev)
+    enc, eoff = codec.encode(src, so, raw_bytes=raw)
+    eo = _u32(eoff)
+    renc, reoff = O.encode_batch(pool, off, nthreads=16)
+    assert np.array_equal(eo, reoff)
+    E = int(eo[-1])
+    assert np.array_equal(enc[:E].cpu().numpy(), renc)
+    dst, doff, st, fs, fl = codec.decode_auto(enc, eoff, enc_bytes=E, want_ctx=True)
+    torch.cuda.synchronize()
+    rd, rdo, rst, rfs, rfl = O.decode_batch(renc, reoff, nthreads=16)
+    assert np.array_equal(st.cpu().numpy(), rst)
+    assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs)
+    assert np.array_equal(fl.cpu().numpy(), rfl)
+    ln = np.diff(off.astype(np.int64))
+    assert np.array_equal(rst, ln)
+    # every decoded byte: the engine slot of string i against the oracle's
+    do = _u32(doff).astype(np.int64)
+    rel = np.arange(raw) - np.repeat(off[:-1].astype(np.int64), ln)
+    d = dst.cpu().numpy()
+    assert np.array_equal(d[np.repeat(do[:-1], ln) + rel],
+                          rd[np.repeat(rdo[:-1].astype(np.int64), ln) + rel])
+
+
+def test_config4_full_16m_one_gpu_properties(codec, dev):
+    """All 16,777,216 config-4 strings (their lengths from the config-4
+    generator; bytes uniform printable ASCII drawn on the GPU) in ONE batch:
+    the encoded and decoded pools stay inside the uint32 offsets; every
+    string decodes to its bytes with status == length and an accepting
+    final state."""
+    import torch
+    from nghttp2_amd import workloads as W
+    lengths = W.mixed_lengths(1 << 24)
+    n = len(lengths)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lengths, out=off[1:])
+    raw = int(off[-1])
+    assert raw < 2 ** 32
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0004)
+    src = torch.randint(0x20, 0x7F, (raw + (-raw) % 16 + 16,), generator=g, device=dev,
+                        dtype=torch.uint8)
+    so = to_dev(off.astype(np.uint32), dev)
+    enc, eoff = codec.encode(src, so, raw_bytes=raw)
+    torch.cuda.synchronize()
+    E = int(eoff[-1].item()) & 0xFFFFFFFF
+    assert E != 0xFFFFFFFF and E > raw // 2
+    dst, doff, st, fs, fl = codec.decode_auto(enc, eoff, enc_bytes=E, want_ctx=True)
+    torch.cuda.synchronize()
+    ln_t = torch.from_numpy(lengths.astype(np.int32)).to(dev)
+    assert torch.equal(st, ln_t)
+    assert bool(((fl & 1) == 1).all())
+    do = doff.to(torch.int64) & 0xFFFFFFFF
+    so64 = so.to(torch.int64) & 0xFFFFFFFF
+    chunk = 1 << 21
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        ln = ln_t[a:b].to(torch.int64)
+        tot = int(ln.sum().item())
+        first = torch.cumsum(ln, 0) - ln
+        rel = torch.arange(tot, device=dev) - torch.repeat_interleave(first, ln)
+        got = dst[torch.repeat_interleave(do[a:b], ln) + rel]
+        want = src[torch.repeat_interleave(so64[a:b], ln) + rel]
+        assert torch.equal(got, want), "strings [%d, %d)" % (a, b)
+
+
+def test_config5_full_size_bit_exact(codec, dev):
+    """BASELINE.json config 5 at full size (1,048,576 strings, seed
+    0x5EED0005): engine slots (decode_auto) and the reference's caller slots
+    (decode), status, final context and every written byte -- including the
+    partial output of the failing strings -- against the oracle."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off, cats = W.gen_adversarial(1 << 20)
+    n, E = len(off) - 1, int(off[-1])
+    rd, rdo, rst, rfs, rfl = O.decode_batch(pool[:E], off, nthreads=16)
+    assert (rst < 0).sum() > 100_000 and (rst >= 0).sum() > 400_000
+    src, so = to_dev(pool, dev), to_dev(off, dev)
+    # the reference's slots, zero-initialised like the oracle's pool: the
+    # whole pool compares, partial outputs included
+    dst = torch.zeros(int(rdo[-1]) + 16, dtype=torch.uint8, device=dev)
+    _, _, st, fs, fl = codec.decode(src, so, dst_off=to_dev(rdo, dev), dst=dst, want_ctx=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), rst)
+    assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs)
+    assert np.array_equal(fl.cpu().numpy(), rfl)
+    assert np.array_equal(dst[:int(rdo[-1])].cpu().numpy(), rd[:int(rdo[-1])])
+    # engine slots: the same results, the decoded bytes of every success
+    d2, doff, st2, fs2, fl2 = codec.decode_auto(src, so, enc_bytes=E, want_ctx=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(st2.cpu().numpy(), rst)
+    assert np.array_equal(fs2.cpu().numpy().view(np.uint16), rfs)
+    assert np.array_equal(fl2.cpu().numpy(), rfl)
+    ok = np.nonzero(rst > 0)[0]
+    ln = rst[ok].astype(np.int64)
+    rel = np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln)
+    do = _u32(doff).astype(np.int64)
+    assert np.array_equal(d2.cpu().numpy()[np.repeat(do[ok], ln) + rel],
+                          rd[np.repeat(rdo[ok].astype(np.int64), ln) + rel])
+
+
+def test_decode_pool_past_4gib_refused(codec, dev):
+    import torch
+    from nghttp2_amd import hd
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(100)
+    src, so = to_dev(pool, dev), to_dev(off, dev)
+    dst = torch.zeros(4096 * 4, dtype=torch.uint8, device=dev)
+    doff = torch.empty(101, dtype=torch.int32, device=dev)
+    st = torch.empty(100, dtype=torch.int32, device=dev)
+    L = hd.lib()
+    rv = L.nghttp2_amd_hd_huff_decode_batch_auto(
+        hd._p(src), hd._p(so), 100, hd._p(dst), (1 << 32) + 64, hd._p(doff), hd._p(st), None,
+        None, hd._stream(None))
+    assert rv == hd.NGHTTP2_ERR_INVALID_ARGUMENT
+
+
+def test_encode_total_past_limit_marks_overflow(codec, dev):
+    """A capacity smaller than the encoded total: no byte past dst_cap, the
+    tiles that fit are encoded exactly, dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(5000, seed=4)
+    renc, reoff = O.encode_batch(pool, off)
+    cap = int(reoff[2600])  # strings past ~2600 do not fit
+    dst = torch.full((cap + 4096,), 0xAB, dtype=torch.uint8, device=dev)
+    eoff = torch.empty(5001, dtype=torch.int32, device=dev)
+    codec.encode(to_dev(pool, dev), to_dev(off, dev), raw_bytes=int(off[-1]),
+                 dst=dst[:cap], dst_off=eoff)
+    torch.cuda.synchronize()
+    eo = _u32(eoff)
+    assert eo[-1] == 0xFFFFFFFF
+    assert (dst[cap:].cpu().numpy() == 0xAB).all()
+    # the first tiles (256 strings each) are whole and exact
+    k = 2560
+    assert np.array_equal(eo[:k + 1], reoff[:k + 1])
+    assert np.array_equal(dst[:int(reoff[k])].cpu().numpy(), renc[:int(reoff[k])])
+
+
+def test_encode_total_past_4gib_marks_overflow(codec, dev):
+    """A real 64-bit total: 1.4 GB of 0xFF bytes (26-bit codes) encode to
+    ~4.5 GB, past the uint32 offsets; the batch reports the overflow and the
+    strings before the limit are exact."""
+    import torch
+    n, L = 1_400_000, 1000
+    raw = n * L
+    off = np.arange(n + 1, dtype=np.int64) * L
+    src = torch.full((raw + 32,), 0xFF, dtype=torch.uint8, device=dev)
+    enc, eoff = codec.encode(src, to_dev(off.astype(np.uint32), dev), raw_bytes=raw)
+    torch.cuda.synchronize()
+    eo = _u32(eoff)
+    assert eo[-1] == 0xFFFFFFFF
+    one, _ = O.encode_batch(np.full(L + 16, 0xFF, np.uint8), np.array([0, L], np.uint32))
+    E1 = len(one)
+    assert E1 == (26 * L + 7) // 8
+    k = 1000  # strings of the first tiles: offsets i * E1 and the same bytes
+    assert np.array_equal(eo[:k + 1].astype(np.int64), np.arange(k + 1) * E1)
+    e = enc[:k * E1].cpu().numpy().reshape(k, E1)
+    assert (e == np.frombuffer(bytes(one), np.uint8)).all()
+    del enc, src
+    torch.cuda.empty_cache()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_gloo_one_gpu(dev):
+    """bench.py's N > 1 path (init, byte-balanced config-4 shard per rank,
+    barrier, max-over-ranks time, summed bytes) as 2 ranks on the one GPU,
+    collectives over gloo."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--config", "4",
+           "--strings", str(1 << 21), "--steps", "3", "--warmup", "1", "--streams", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["value"] > 0
+    # the two shards cover the set: 2 * strings_per_gpu is about 2M
+    assert abs(2 * out["config"]["strings_per_gpu"] - (1 << 21)) < 4096
+
+
+def test_compat_per_call_latency(dev):
+    """The link-level drop-in (one string per call, as emit_string and
+    hd_inflate_read_huff call it) against the port, per call; results equal.
+    The numbers go to gpurun_out/compat_latency.json for INTEGRATION.md."""
+    import tempfile
+    libdir = os.path.join(REPO, "nghttp2_amd", "lib")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "compat_latency")
+        subprocess.run(["gcc", "-O2", "-Wall", "-I", os.path.join(REPO, "include"),
+                        os.path.join(REPO, "tests", "c", "compat_latency.c"), "-L" + libdir,
+                        "-lnghttp2_amd_hd", "-Wl,-rpath," + libdir, "-ldl", "-o", exe], check=True)
+        r = subprocess.run([exe, O.lib_path() if hasattr(O, "lib_path") else
+                            os.path.join(REPO, "oracle", "_build", "libhuff_oracle.so"), "2000"],
+                           capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["mismatches"] == 0
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "compat_latency.json"), "w") as f:
+        json.dump(res, f)
+    print(res)
