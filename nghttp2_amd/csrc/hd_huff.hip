@@ -56,7 +56,7 @@ namespace host {
 // kept in SGPRs, one row per wave written once at exit).  Slots: 0 task
 // setup, 1 staging, 2 pass 1, 3 verify, 4 scan, 5 pass 2, 6 round end,
 // 7 lifetime, 8 tasks, 9 rounds.
-__device__ unsigned long long g_stamps[4096][16];
+__device__ unsigned long long g_stamps[4096][20];
 #define WSTAMP(slot)                                                           \
   do {                                                                         \
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime();               \
@@ -64,19 +64,38 @@ __device__ unsigned long long g_stamps[4096][16];
     wt0 = t1_;                                                                 \
   } while (0)
 #define WCOUNT(slot) (++wst[slot])
-#define WSTAMP_INIT() unsigned long long wst[10] = {}, wt0 = __builtin_amdgcn_s_memtime(), wbirth = wt0
-#define WSTAMP_FLUSH()                                                         \
+#define WSTAMP_INIT() unsigned long long wst[13] = {}, wt0 = __builtin_amdgcn_s_memtime(), wbirth = wt0
+#define WSTAMP_FLUSH() WSTAMP_FLUSH_W(DEC_WAVES)
+#define WSTAMP_FLUSH_W(NW)                                                     \
   do {                                                                         \
     wst[7] = __builtin_amdgcn_s_memtime() - wbirth;                            \
-    if (lane == 0)                                                             \
-      for (int s_ = 0; s_ < 10; ++s_) g_stamps[(blockIdx.x * DEC_WAVES + wv) & 4095][s_] = wst[s_]; \
+    unsigned long long c_[4];                                                  \
+    for (int k_ = 0; k_ < 4; ++k_) {                                           \
+      unsigned long long t_ = 0;                                               \
+      for (int l_ = 0; l_ < 64; ++l_) t_ += __builtin_amdgcn_readlane(dctr[k_], l_); \
+      c_[k_] = t_;                                                             \
+    }                                                                          \
+    if (lane == 0) {                                                           \
+      for (int s_ = 0; s_ < 13; ++s_) g_stamps[(blockIdx.x * (NW) + wv) & 4095][s_] = wst[s_]; \
+      for (int k_ = 0; k_ < 4; ++k_) g_stamps[(blockIdx.x * (NW) + wv) & 4095][13 + k_] = c_[k_]; \
+    }                                                                          \
   } while (0)
-#define DCTR(k) (++dctr[k])
+// counts wave iterations: only the first active lane counts (the flush sums lanes)
+#define DCTR(k)                                                                \
+  do {                                                                         \
+    const uint32_t l_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); \
+    if (__builtin_amdgcn_readfirstlane(l_) == l_) ++dctr[k];                   \
+  } while (0)
+#define DD_SARGS , unsigned long long *wst, unsigned long long &wt0
+#define DD_SPASS , wst, wt0
 #else
+#define DD_SARGS
+#define DD_SPASS
 #define WSTAMP(slot) do { } while (0)
 #define WCOUNT(slot) do { } while (0)
 #define WSTAMP_INIT() do { } while (0)
 #define WSTAMP_FLUSH() do { } while (0)
+#define WSTAMP_FLUSH_W(NW) do { } while (0)
 #define DCTR(k) do { } while (0)
 #endif
 
@@ -1142,7 +1161,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
   WSTAMP_INIT();
   const uint32_t off0 = off[0];
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
-  uint32_t dctr[3] = {0, 0, 0};
+  uint32_t dctr[4] = {0, 0, 0, 0};
   (void)dctr;
   for (uint32_t task = blockIdx.x * DEC_WAVES + wv; task < ntask; task += gridDim.x * DEC_WAVES) {
     const uint32_t t0 = task * TASK_STR;
@@ -1346,6 +1365,805 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
+// Dense decode (decode_batch_auto): byte-balanced pieces across string
+// boundaries, output staged in LDS and written back to back.
+// ---------------------------------------------------------------------------
+// A wave owns a task of TASK_STR consecutive strings and walks their encoded
+// bytes [A, Z) in rounds of 64 pieces of DD_P bytes, one piece per lane,
+// whatever the string boundaries, so every lane of a round has the same
+// amount of input.  Lane l's piece [s, e) holds:
+//   seg0   the string running into it (if s is not a string start): entry
+//          at the first codeword boundary >= 8 s (or the string's tail),
+//          found by a warm-up decode from max(string start, s - DD_OV) --
+//          exact when the warm-up starts at the string start, else
+//          speculative and verified against the previous lane's exit
+//          (mismatches are re-decoded from it, so the result is exact);
+//   rest   every string starting in [s, e), decoded exactly from its start.
+// A segment decodes to the first boundary >= 8 e or to its string's end.
+// The string ending in a piece is finished by that piece's lane: the status
+// of seg0's string needs the symbols of the lanes before (a segmented scan
+// over lanes); the others are complete in the lane.
+// Symbols go to the lane's LDS output region, seg0 first; after the round
+// a plain scan of the lanes' byte counts places every region at the task's
+// running output count and each lane stores its bytes (dword stores, the
+// unaligned ends bytewise).  The task's output is dense from its base
+// auto_slot(x_t0, t0): string j at dst_off[j], the strings of a task back to
+// back, so HBM sees the decoded bytes once (no slot gaps).
+#ifndef DD_P
+#define DD_P 32u   // piece bytes per lane
+#endif
+#ifndef DD_OV
+#define DD_OV 24u  // warm-up bytes of a later item
+#endif
+#ifndef DD_WAVES
+#define DD_WAVES 14  // waves per workgroup: one lookup table per CU
+#endif
+#ifndef DD_SKEW
+#define DD_SKEW 0  // staged input: a copy of the next block's first dword after every 8
+#endif
+#ifndef DD_ABL_NOSTORE
+#define DD_ABL_NOSTORE 0  // ablation build only (tools/diag): no output stores
+#endif
+#ifndef DD_BB
+#define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
+#endif
+#define DD_NT (WAVE * DD_WAVES)
+// a lane decodes bits [8 s, 8 e + 29] at most: <= (8 P + 29) / 5 symbols,
+// plus one byte of slack (the second byte of a 1-symbol entry is written)
+#define DD_RB ((((8u * DD_P + 29u) / 5u) + 2u + 3u) & ~3u)
+#define DD_IBL ((WAVE * DD_P + DD_OV + 64u) / 4u + 8u)          // staged dwords (logical)
+#define DD_PF ((WAVE * DD_P + DD_OV + 8u + 32u + 16u * WAVE - 1u) / (16u * WAVE))  // staged chunks per lane
+#define DD_IBW (DD_SKEW ? DD_IBL + DD_IBL / 8u + 2u : DD_IBL)   // physical
+
+struct DDShared {
+  DecTables T;  // first: the lookup at LDS offset 0
+  uint32_t ib[DD_WAVES][DD_IBW];
+  uint32_t ob[DD_WAVES][WAVE * DD_RB / 4 + 1];
+  uint32_t ostart[DD_WAVES][TASK_STR];  // string output starts (task-relative)
+  uint32_t sa[DD_WAVES][TASK_STR + 1];  // the task's string starts, then its end Z
+};
+
+// Decode symbols into a byte stream in LDS: both bytes of an entry are
+// written, the count advances by the entry's symbols.
+struct DIShared {  // k_decode_items
+  DecTables T;  // first: the lookup at LDS offset 0
+  uint32_t ib[DD_WAVES][DD_IBW];
+  uint32_t ob[DD_WAVES][WAVE * DD_RB / 4 + 1];
+  uint32_t ostart[DD_WAVES][TASK_STR];  // string output starts (task-relative)
+  uint32_t smap[DD_WAVES][WAVE];        // a round's items -> strings (1-based, max-scanned)
+};
+
+struct DiscardSink {  // a warm-up: its symbols belong to the item before
+  __device__ __forceinline__ uint32_t count() const { return 0; }
+  __device__ __forceinline__ void put_nf(uint32_t, uint32_t) {}
+  __device__ __forceinline__ void put(uint32_t, uint32_t) {}
+  __device__ __forceinline__ void flush() {}
+};
+
+struct LdsSink {
+  lds_u8 *p;
+  uint32_t n;
+  __device__ __forceinline__ uint32_t count() const { return n; }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    p[n] = (uint8_t)v;
+    p[n + 1] = (uint8_t)(v >> 8);
+    n += c8 >> 3;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
+  __device__ __forceinline__ void flush() {}
+};
+
+// Staged input, skewed: logical dword k lives at k + k / 8, and each block of
+// 8 is followed by a copy of the next block's first dword, so the two dwords
+// of a window are adjacent while the 64 lanes' pieces (8 dwords apart for
+// 32-byte pieces) fall on different LDS banks.
+__device__ __forceinline__ uint32_t dd_phys(uint32_t k) { return DD_SKEW ? k + (k >> 3) : k; }
+__device__ __forceinline__ uint32_t dd_win(const lds_u32 *ib, uint32_t q) {  // q = bp - 1
+  const uint32_t p = dd_phys(q >> 5);
+  return __builtin_amdgcn_alignbit(ib[p], ib[p + 1], ~q);
+}
+
+struct DDRun {
+  bool failed, at_end;
+  uint32_t t, win;  // at the string end: tail bits and the last window
+};
+
+// Decode from bp (advanced in place) to the first codeword boundary >=
+// bstop, or to the string end bend (tail analysis), into sink.
+//
+// Fast steps come from a register bit buffer: bb holds the stream's bits
+// [bp, 32 k) MSB first (nb of them, >= 32 at a step's start), refilled
+// without a branch from the staged dword k (prefetched in nxt), so a step's
+// only dependent memory access is its lookup.  A fast step needs its 14
+// lookup bits inside the string (bp + 14 <= bend) and must not pass the
+// first boundary >= bstop (bp <= bstop - 13: the first symbol of a 2-symbol
+// entry is <= 9 bits); pairs run while both steps qualify.  A code longer
+// than the lookup (entry 0) stalls the lane for the rest of the pair, then
+// goes through slow_entry; one that would pass the string end is its tail
+// and leaves the fast loop.  The last bits go through checked steps (LDS
+// windows), which also settle the tail: the undecoded t < 30 bits.
+#define DD_REFILL()                                                      \
+  do {                                                                   \
+    const bool t_ = nb < 32u;                                            \
+    bb |= (uint64_t)(t_ ? nxt : 0u) << ((32u - nb) & 63u);               \
+    nb += t_ ? 32u : 0u;                                                 \
+    k += t_ ? 1u : 0u;                                                   \
+    nxt = ib[dd_phys(k)];                                                \
+  } while (0)
+template <class Sink>
+__device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, uint32_t &bp,
+                                        uint32_t bstop, uint32_t bend, Sink &sink,
+                                        uint32_t *dctr DD_SARGS) {
+  (void)dctr;
+  WSTAMP(2);  // (the caller's bookkeeping)
+  DDRun r;
+  r.at_end = false;
+  r.t = 0;
+  r.win = 0;
+  bool failed = false;
+  int32_t G2 = min((int32_t)bstop - 27, (int32_t)bend - 28);  // last start of a fast pair
+  uint32_t k = bp >> 5;
+  const uint32_t o = bp & 31u;
+  const uint32_t w0 = ib[dd_phys(k)], w1 = ib[dd_phys(k + 1u)];
+  uint64_t bb = (((uint64_t)w0 << 32) | w1) << o;
+  uint32_t nb = 64u - o;
+  k += 2u;
+  uint32_t nxt = ib[dd_phys(k)];
+  // a code longer than the lookup inside the pair loop (nb >= 32): decode
+  // it, or leave the pair loop at EOS (failed) or at the string's tail
+  // (the careful steps find it again)
+#define DD_SLOW()                                                        \
+  do {                                                                   \
+    const uint32_t rem_ = bend - bp;                                     \
+    const uint32_t e_ = slow_entry(T, (uint32_t)(bb >> 32), rem_);       \
+    if (e_ == 0xFFFFFFFFu) {                                             \
+      failed = true;                                                     \
+      G2 = INT32_MIN;                                                    \
+    } else if (E_L1(e_) > rem_) {                                        \
+      G2 = INT32_MIN;                                                    \
+    } else {                                                             \
+      sink.put(e_ & 0xFFFFu, E_CNT8(e_));                                \
+      const uint32_t U_ = E_USED(e_);                                    \
+      bb <<= U_;                                                         \
+      bp += U_;                                                          \
+      nb -= U_;                                                          \
+      DD_REFILL();                                                       \
+    }                                                                    \
+  } while (0)
+  while ((int32_t)bp <= G2) {
+    DCTR(0);
+    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - HD_HUFF_LUT_BITS)];
+    sink.put_nf(e1 & 0xFFFFu, E_CNT8(e1));
+    const uint32_t U1 = E_USED(e1);
+    bb <<= U1;
+    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - HD_HUFF_LUT_BITS)];
+    sink.put_nf(e2 & 0xFFFFu, E_CNT8(e2));
+    const uint32_t U2 = E_USED(e2);
+    bb <<= U2;
+    bp += U1 + U2;
+    nb -= U1 + U2;
+    DD_REFILL();
+    if (e2 == 0u) DD_SLOW();  // (an e1 of 0 stalls e2 too)
+  }
+#undef DD_SLOW
+  WSTAMP(10);
+  // careful steps: each one predicated on the stop rules instead of branching
+  // -- a step takes its first symbol only if the code ends inside the string
+  // (L1 <= rem), its second only if that one does too and the first ended
+  // before bstop; a first code that does not fit is the string's tail
+  bool done = failed;
+  while (__ballot(!done)) {
+    if (!done) {
+      DCTR(2);
+      const uint32_t w = (uint32_t)(bb >> 32);
+      const uint32_t rem = bend - bp;
+      const bool stop = bp >= bstop || rem == 0u;
+      uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
+      if (e == 0u && !stop) e = slow_entry(T, w, rem);
+      if (e == 0xFFFFFFFFu) {
+        failed = true;  // EOS: the sticky failure state
+        done = true;
+      } else {
+        const uint32_t L1 = E_L1(e), U = E_USED(e);
+        const bool take1 = !stop && L1 <= rem;
+        const bool take2 = take1 && E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
+        if (!stop && !take1) {  // the tail: a proper prefix of a code
+          r.at_end = true;
+          r.t = rem;
+          r.win = w;
+        }
+        const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
+        sink.put(take2 ? (e & 0xFFFFu) : (e & 0xFFu), take2 ? 16u : (take1 ? 8u : 0u));
+        bb <<= adv;
+        bp += adv;
+        nb -= adv;
+        DD_REFILL();
+        done = !take1 || bp >= bstop;
+      }
+    }
+  }
+  WSTAMP(11);
+  if (!failed && bp == bend) r.at_end = true;
+  r.failed = failed;
+  WSTAMP(12);
+  return r;
+}
+#undef DD_REFILL
+
+// Status and final decode context of a string (lib/nghttp2_hd_huffman.c:
+// 135-142) from its tail: as finish_string, with the FSM state (three table
+// reads) only when the caller asked for it.
+__device__ __forceinline__ void dd_finish(const DecTables &T, bool failed, uint32_t t,
+                                          uint32_t win, uint32_t nsym, bool ovf, uint32_t j,
+                                          int32_t *status, uint16_t *fstate_out,
+                                          uint8_t *flags_out) {
+  const uint32_t v = t ? (win >> (32 - t)) : 0u;
+  const bool accept = !failed && (t <= 7) && (v == (1u << t) - 1u);
+  status[j] = ovf ? NGHTTP2_AMD_ERR_BUFFER_ERROR
+                  : (accept ? (int32_t)nsym : NGHTTP2_AMD_ERR_HEADER_COMP);
+  if (fstate_out) {
+    fstate_out[j] = failed ? (uint16_t)FAIL_STATE
+                           : (uint16_t)(t ? T.depth_ids[T.depth_base[t] + (v - T.depth_lo[t])] : 0u);
+    flags_out[j] = failed ? 0u
+                          : (uint8_t)((accept ? HUFF_ACCEPTED : 0u) | ((t < 4 && nsym) ? HUFF_SYM : 0u));
+  }
+}
+
+#define DD_NONE 0xFFFFFFFCu  // exit: the lane's last string ended in its piece
+enum { DD_WARM = 0, DD_SEG0 = 1, DD_REST = 2, DD_DONE = 3 };
+
+__global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restrict__ src,
+                                                        const uint32_t *__restrict__ off,
+                                                        uint32_t n, uint8_t *__restrict__ dst,
+                                                        uint64_t dst_cap,
+                                                        uint32_t *__restrict__ dst_off,
+                                                        int32_t *__restrict__ status,
+                                                        uint16_t *__restrict__ fstate_out,
+                                                        uint8_t *__restrict__ flags_out) {
+  __shared__ DDShared S;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lds_u32 *ibw = (lds_u32 *)S.ib[wv];
+  const lds_u32 *ibe = ibw;
+  lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * DD_RB;
+  const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
+  lds_u32 *ost = (lds_u32 *)S.ostart[wv];
+  lds_u32 *sa = (lds_u32 *)S.sa[wv];
+  stage_dec_tables(S.T, DD_NT);  // the kernel's only workgroup barrier
+  WSTAMP_INIT();
+  const uint32_t off0 = off[0];
+  const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
+  uint32_t dctr[4] = {0, 0, 0, 0};
+  (void)dctr;
+  for (uint32_t task = blockIdx.x * DD_WAVES + wv; task < ntask; task += gridDim.x * DD_WAVES) {
+    WCOUNT(8);
+    const uint32_t t0 = task * TASK_STR;
+    const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
+    const bool sl = lane < nstr;
+    const uint32_t a_l = sl ? off[t0 + lane] : 0xFFFFFFFFu;
+    const uint32_t b_l = sl ? off[t0 + lane + 1] : 0xFFFFFFFFu;
+    const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+    const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
+    const uint64_t tbase = auto_slot(A - off0, t0);
+    // a string whose slot bound passes dst_cap reports -502 (monotone in j;
+    // checked per string only in a task that reaches past dst_cap)
+    const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
+    const bool ovf_l = sl && task_ovf && auto_slot(b_l - off0, t0 + lane + 1u) > dst_cap;
+    ost[lane] = 0xFFFFFFFFu;
+    if (sl) sa[lane] = a_l;
+    if (lane == 0) sa[nstr] = Z;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
+    for (uint32_t R = A; R < Z; R += WAVE * DD_P) {
+      const uint32_t s = R + lane * DD_P;
+      const bool valid = s < Z;
+      const uint32_t e = min(s + DD_P, Z);
+      const uint32_t nv = min((Z - R + DD_P - 1u) / DD_P, (uint32_t)WAVE);
+      // lb = the strings starting before s (task strings are contiguous and
+      // ordered, empty ones included); string lb - 1 holds byte s when it
+      // ends past s
+      uint32_t lb = 0;
+#pragma unroll
+      for (uint32_t st = 32; st; st >>= 1)
+        if (lb + st <= nstr && sa[lb + st - 1u] < s) lb += st;
+      if (lb < nstr && sa[lb] < s) ++lb;
+      const uint32_t j0 = lb ? lb - 1u : 0u;
+      const uint32_t a0 = sa[j0], b0 = sa[j0 + 1u];
+      const bool mid = valid && lb > 0 && b0 > s;  // the piece starts inside string j0
+      WCOUNT(9);
+      WSTAMP(0);
+      // ---- stage [max(A, R - OV), min(R + 64 P, Z) + 8) (aligned 16-byte chunks)
+      const uint32_t lo = (R - A > DD_OV ? R - DD_OV : A);
+      const uint32_t IB = lo & ~15u;
+      const uint32_t IBX = IB - 16u;
+      {
+        const uint32_t hi = min(R + WAVE * DD_P, Z) + 8u;
+        const uint32_t nchunk = (((hi + 15u) & ~15u) - IB) >> 4;
+        const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
+        for (uint32_t c = lane; c < nchunk; c += WAVE) {
+          const uint4 v = g[c];
+          const uint32_t k = 4u * c + 4u;  // logical dword (4 spare dwords first)
+          const uint32_t p = dd_phys(k);   // the chunk's 4 dwords stay in one block
+          ibw[p] = __builtin_bswap32(v.x);
+          ibw[p + 1] = __builtin_bswap32(v.y);
+          ibw[p + 2] = __builtin_bswap32(v.z);
+          ibw[p + 3] = __builtin_bswap32(v.w);
+          if (DD_SKEW && (k & 7u) == 0u) ibw[p - 1] = __builtin_bswap32(v.x);  // the copy
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      WSTAMP(1);
+      if (carry_exit < DD_NONE) carry_exit -= 8u * (IB - IB_prev);
+      IB_prev = IB;
+      const uint32_t bs = 8u * (s - IBX), bE = 8u * (e - IBX);
+      // ---- one decode loop per lane over its piece: seg0's warm-up, seg0,
+      // then the strings starting in the piece.  The wave runs the loop while
+      // any lane has a segment left, so lanes in different segments share
+      // the same decode steps.
+      const bool fin0 = mid && b0 <= e;  // seg0's string ends in this piece
+      const uint32_t bend0 = 8u * (min(b0, e + 8u) - IBX);
+      const uint32_t bstop0 = fin0 ? bend0 : bE;
+      const bool exact0 = !mid || a0 + DD_OV >= s;
+      SubOut r0;
+      r0.entry = r0.exit = DD_NONE;
+      r0.cnt = 0;
+      r0.t = r0.win = 0;
+      r0.at_end = false;
+      LdsSink sk;
+      sk.p = my_ob;
+      sk.n = 0;
+      uint32_t mode = !valid ? DD_DONE : (mid ? DD_WARM : DD_REST);
+      uint32_t bp = 0, bstop = 0, bend = 0;
+      uint32_t j = lb, c_before = 0, cnt0 = 0;
+      uint32_t tail_exit = DD_NONE, tail_cnt = 0;
+      bool head = false;  // a string starts in this piece
+      if (mode == DD_WARM) {
+        bp = 8u * ((exact0 ? a0 : s - DD_OV) - IBX);
+        bstop = bs;
+        bend = bend0;
+      }
+      // next rest string: empty ones are finished on the spot
+      auto next_string = [&]() {
+        while (j < nstr && sa[j] < e) {
+          const uint32_t a = sa[j], b = sa[j + 1u];
+          head = true;
+          ost[j] = sk.n - cnt0;  // relative to the rest's first byte (fixed after the scan)
+          if (a != b) {
+            bp = 8u * (a - IBX);
+            bend = 8u * (min(b, e + 8u) - IBX);
+            bstop = b <= e ? bend : bE;
+            c_before = sk.n;
+            mode = DD_REST;
+            return;
+          }
+          dd_finish(S.T, false, 0, 0, 0, task_ovf && auto_slot(b - off0, t0 + j + 1u) > dst_cap,
+                    t0 + j, status, fstate_out, flags_out);
+          ++j;
+        }
+        mode = DD_DONE;
+      };
+      if (mode == DD_REST) next_string();
+      while (__ballot(mode != DD_DONE)) {
+        WCOUNT(6);
+        if (mode != DD_DONE) {
+          const DDRun rr = dd_run(S.T, ibe, bp, bstop, bend, sk, dctr DD_SPASS);
+          if (mode == DD_WARM) {
+            // the entry: the first boundary >= 8 s, or the string's tail
+            sk.n = 0;  // the warm-up's symbols belong to the lane before
+            if (rr.failed) {  // EOS before s: known failed if exact
+              r0.entry = r0.exit = exact0 ? XFAIL : XUNKNOWN;
+              cnt0 = 0;
+              j = lb;
+              next_string();
+            } else {
+              r0.entry = bp;
+              bstop = bstop0;
+              mode = DD_SEG0;
+            }
+          } else if (mode == DD_SEG0) {
+            r0.exit = rr.failed ? XFAIL : bp;
+            r0.at_end = rr.at_end;
+            r0.t = rr.t;
+            r0.win = rr.win;
+            cnt0 = sk.n;
+            r0.cnt = cnt0;
+            j = lb;
+            next_string();
+          } else {  // DD_REST: string j
+            const uint32_t b = sa[j + 1u];
+            if (b <= e) {  // it ends in this piece: finished
+              dd_finish(S.T, rr.failed, rr.t, rr.win, sk.n - c_before,
+                        task_ovf && auto_slot(b - off0, t0 + j + 1u) > dst_cap, t0 + j, status,
+                        fstate_out, flags_out);
+              tail_exit = DD_NONE;
+              tail_cnt = 0;
+              ++j;
+              next_string();
+            } else {  // it runs into the next piece: the lane's open tail
+              tail_exit = rr.failed ? XFAIL : bp;
+              tail_cnt = sk.n - c_before;
+              ++j;
+              mode = DD_DONE;
+            }
+          }
+        }
+      }
+      const uint32_t jr1 = j;  // rest strings [lb, jr1)
+      const uint32_t rest_n = sk.n - cnt0;
+      WSTAMP(2);
+      // ---- verify seg0 against the previous lane's exit; re-decode mismatches
+      uint32_t my_exit = head ? tail_exit : (mid && !fin0 ? r0.exit : DD_NONE);
+      uint32_t c0 = cnt0;
+      for (uint32_t iter = 0; iter <= WAVE; ++iter) {
+        const uint32_t up = __shfl_up(my_exit, 1, 64);
+        const uint32_t pred = lane ? up : carry_exit;
+        const bool mism = mid && !exact0 && (r0.entry != pred || r0.entry == XUNKNOWN);
+        const uint64_t bal = __ballot(mism);
+        if (bal == 0) break;
+        const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
+        if (mism && !pred_mism) {
+          // re-decode seg0 from the settled exit (a warm-up that did not
+          // synchronise); the rest's bytes wait at the region's end meanwhile
+          // (backward copy: the target lies past the source)
+          for (uint32_t k = rest_n; k-- > 0;) my_ob[DD_RB - rest_n + k] = my_ob[c0 + k];
+          LdsSink s3;
+          s3.p = my_ob;
+          s3.n = 0;
+          if (pred == XFAIL || pred == XUNKNOWN || pred == DD_NONE) {
+            r0.entry = r0.exit = XFAIL;  // the string failed before this piece
+            r0.cnt = 0;
+            r0.t = r0.win = 0;
+            r0.at_end = false;
+          } else {
+            uint32_t bq = pred;
+            const DDRun rr = dd_run(S.T, ibe, bq, bstop0, bend0, s3, dctr DD_SPASS);
+            r0.entry = pred;
+            r0.exit = rr.failed ? XFAIL : bq;
+            r0.t = rr.t;
+            r0.win = rr.win;
+            r0.at_end = rr.at_end;
+            r0.cnt = s3.n;
+          }
+          for (uint32_t k = 0; k < rest_n; ++k) my_ob[s3.n + k] = my_ob[DD_RB - rest_n + k];
+          c0 = s3.n;
+          if (!head && !fin0) my_exit = r0.exit;
+        }
+      }
+      WSTAMP(3);
+      // ---- seg0's running symbol count: segmented scan over the lanes (heads:
+      // pieces where a string starts); V = the count of the lane's open tail
+      const uint32_t V = valid ? (head ? tail_cnt : c0) : 0u;
+      const bool H = !valid || head;
+      uint32_t ps = V;
+      int32_t hm = H ? (int32_t)lane : -1;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o2 = __shfl_up(ps, d, 64);
+        const int32_t oh = __shfl_up(hm, d, 64);
+        if (lane >= d) {
+          ps += o2;
+          hm = max(hm, oh);
+        }
+      }
+      const uint32_t excl_h = __shfl(ps - V, hm >= 0 ? (uint32_t)hm : 0u, 64);
+      const uint32_t seg = hm >= 0 ? ps - excl_h : ps + carry_cnt;  // inclusive
+      const uint32_t seg_prev_up = __shfl_up(seg, 1, 64);
+      const uint32_t seg_prev = lane ? seg_prev_up : carry_cnt;
+      if (fin0) {  // seg0's string ends here
+        dd_finish(S.T, r0.exit == XFAIL || r0.entry == XFAIL, r0.t, r0.win, seg_prev + c0,
+                  task_ovf && auto_slot(b0 - off0, t0 + j0 + 1u) > dst_cap, t0 + j0, status,
+                  fstate_out, flags_out);
+      }
+      // ---- place the lanes' bytes: plain scan of the byte counts
+      const uint32_t T_l = valid ? c0 + rest_n : 0u;
+      const uint32_t Tinc = wave_incl_scan(T_l);
+      const uint32_t O_l = run + Tinc - T_l;  // task-relative
+      for (uint32_t jj = lb; jj < jr1; ++jj) ost[jj] += O_l + c0;
+      WSTAMP(4);
+      // ---- store [tbase + O_l, + T_l) from the region: the bytes before the
+      // first aligned dword, then dwords (two region dwords, one alignbyte),
+      // then the tail bytes; nothing at or past dst_cap is written (strings
+      // past it are -502)
+      if (T_l && !DD_ABL_NOSTORE) {
+        const uint64_t g0 = tbase + O_l;
+        const uint32_t h = min((uint32_t)((4u - (g0 & 3u)) & 3u), T_l);  // head bytes
+        for (uint32_t k = 0; k < h; ++k)
+          if (g0 + k < dst_cap) dst[g0 + k] = my_ob[k];
+        uint32_t k = h;
+        for (; k + 4u <= T_l; k += 4u) {
+          const uint32_t w = k >> 2;
+          const uint32_t v = __builtin_amdgcn_alignbyte(my_ob32[w + 1u], my_ob32[w], h);
+          if (g0 + k + 4u <= dst_cap) *reinterpret_cast<uint32_t *>(dst + g0 + k) = v;
+        }
+        for (; k < T_l; ++k)
+          if (g0 + k < dst_cap) dst[g0 + k] = my_ob[k];
+      }
+      WSTAMP(5);
+      run += __builtin_amdgcn_readlane(Tinc, 63);
+      carry_exit = __builtin_amdgcn_readlane(my_exit, nv - 1u);
+      carry_cnt = __builtin_amdgcn_readlane(seg, nv - 1u);
+      // the next round overwrites the staged input and the regions
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- epilogue: output starts (dst_off); empty strings at the task's end
+    if (sl) {
+      uint32_t o = ost[lane];
+      if (o == 0xFFFFFFFFu) {  // an empty string at Z (or an all-empty task)
+        o = run;
+        dd_finish(S.T, false, 0, 0, 0, ovf_l, t0 + lane, status, fstate_out, flags_out);
+      }
+      dst_off[t0 + lane] = (uint32_t)min(tbase + o, dst_cap);
+      if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase + run, dst_cap);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  WSTAMP_FLUSH_W(DD_WAVES);
+}
+
+// ---------------------------------------------------------------------------
+// Dense decode by items (decode_batch_auto): a string of <= DD_P encoded
+// bytes is one item, a longer one is cut into items of DD_P bytes; a wave
+// takes 64 consecutive items per round, one per lane, so no lane ever
+// crosses a string end.  A string's first item decodes exactly from the
+// string start; a later item warms up from DD_OV bytes before its start to
+// the first codeword boundary at or after it (verified against the previous
+// item's exit, re-decoded on a mismatch).  Symbols go to the lane's LDS
+// region; a segmented scan over the items gives each string's symbol count
+// (status), a plain scan of the lanes' byte counts places the regions back
+// to back from the task's base, and each lane stores its bytes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restrict__ src,
+                                                        const uint32_t *__restrict__ off,
+                                                        uint32_t n, uint8_t *__restrict__ dst,
+                                                        uint64_t dst_cap,
+                                                        uint32_t *__restrict__ dst_off,
+                                                        int32_t *__restrict__ status,
+                                                        uint16_t *__restrict__ fstate_out,
+                                                        uint8_t *__restrict__ flags_out) {
+  __shared__ DIShared S;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lds_u32 *ibw = (lds_u32 *)S.ib[wv];
+  const lds_u32 *ibe = ibw;
+  lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * DD_RB;
+  const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
+  lds_u32 *ost = (lds_u32 *)S.ostart[wv];
+  stage_dec_tables(S.T, DD_NT);  // the kernel's only workgroup barrier
+  WSTAMP_INIT();
+  const uint32_t off0 = off[0];
+  const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
+  uint32_t dctr[4] = {0, 0, 0, 0};
+  (void)dctr;
+  for (uint32_t task = blockIdx.x * DD_WAVES + wv; task < ntask; task += gridDim.x * DD_WAVES) {
+    WCOUNT(8);
+    const uint32_t t0 = task * TASK_STR;
+    const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
+    const bool sl = lane < nstr;
+    const uint32_t a_l = sl ? off[t0 + lane] : 0u;
+    const uint32_t b_l = sl ? off[t0 + lane + 1] : 0u;
+    const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+    const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
+    const uint64_t tbase = auto_slot(A - off0, t0);
+    const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
+    // items: m_l of string l, X_l the first
+    const uint32_t m_l = sl ? max(1u, (b_l - a_l + DD_P - 1u) / DD_P) : 0u;
+    const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
+    const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
+    uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
+    // the staged range of a round whose items start at byte R0 (a round's
+    // items are contiguous in the pool, the next one starting where the last
+    // one ends): [IB, IB + 16 nchunk) = [R0 - OV, min(R0 + 64 P, Z) + 8)
+    // (clipped to the task, aligned)
+    auto round_range = [&](uint32_t R0, uint32_t &IBo, uint32_t &nchunk) {
+      IBo = (R0 - A > DD_OV ? R0 - DD_OV : A) & ~15u;
+      nchunk = (((min(R0 + WAVE * DD_P, Z) + 8u + 15u) & ~15u) - IBo) >> 4;
+    };
+    lds_u32 *smap = (lds_u32 *)S.smap[wv];
+    uint32_t R0 = A;
+    // the next round's input is loaded into registers during this round
+    uint4 pf[DD_PF];
+    uint32_t pf_IB = 0xFFFFFFFFu;
+    for (uint32_t r0 = 0; r0 < M; r0 += WAVE) {
+      const uint32_t nv = min(M - r0, (uint32_t)WAVE);
+      const uint32_t q = r0 + lane;
+      const bool valid = lane < nv;
+      // this lane's item: its string i = the last one with X_i <= q; every
+      // string with an item in the round marks its first one (or item 0 of
+      // the round), then a max-scan over the lanes
+      smap[lane] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (sl && P_l > r0 && X_l < r0 + WAVE) smap[X_l > r0 ? X_l - r0 : 0u] = lane + 1u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t i = min(wave_incl_max(smap[lane]), nstr) - 1u;
+      const uint32_t k = q - __shfl(X_l, i, 64);
+      const uint32_t a = __shfl(a_l, i, 64), b = __shfl(b_l, i, 64);
+      const uint32_t s = a + DD_P * k, e = min(b, s + DD_P);
+      const bool last = e == b;
+      const bool spec = valid && k > 0;
+      WCOUNT(9);
+      WSTAMP(0);
+      // ---- stage [first item (- OV), last item's end + 8)
+      uint32_t IB, nchunk;
+      round_range(R0, IB, nchunk);
+      const uint32_t IBX = IB - 16u;
+      {
+        const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
+        if (pf_IB != IB) {  // (the task's first round)
+#pragma unroll
+          for (uint32_t u = 0; u < DD_PF; ++u)
+            if (lane + WAVE * u < nchunk) pf[u] = g[lane + WAVE * u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < DD_PF; ++u) {
+          const uint32_t c = lane + WAVE * u;
+          if (c < nchunk) {
+            const uint32_t p = dd_phys(4u * c + 4u);
+            ibw[p] = __builtin_bswap32(pf[u].x);
+            ibw[p + 1] = __builtin_bswap32(pf[u].y);
+            ibw[p + 2] = __builtin_bswap32(pf[u].z);
+            ibw[p + 3] = __builtin_bswap32(pf[u].w);
+            if (DD_SKEW && (c & 1u) == 1u) ibw[p - 1] = __builtin_bswap32(pf[u].x);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // prefetch the next round of this task
+        pf_IB = 0xFFFFFFFFu;
+        if (r0 + WAVE < M) {
+          uint32_t IBn, ncn;
+          round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), IBn, ncn);
+          const uint4 *gn = reinterpret_cast<const uint4 *>(src + IBn);
+#pragma unroll
+          for (uint32_t u = 0; u < DD_PF; ++u)
+            if (lane + WAVE * u < ncn) pf[u] = gn[lane + WAVE * u];
+          pf_IB = IBn;
+        }
+      }
+      WSTAMP(1);
+      if (carry_exit < DD_NONE) carry_exit -= 8u * (IB - IB_prev);
+      IB_prev = IB;
+      const uint32_t bs = 8u * (s - IBX);
+      const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
+      const uint32_t bstop = last ? bend : 8u * (e - IBX);
+      LdsSink sk;
+      sk.p = my_ob;
+      sk.n = 0;
+      // ---- warm-up of the later items: to the first boundary >= 8 s
+      uint32_t entry = bs;
+      bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
+      if (spec) {
+        uint32_t bp = 8u * (s - DD_OV - IBX);
+        DiscardSink dk;
+        const DDRun rw = dd_run(S.T, ibe, bp, bs, bend, dk, dctr DD_SPASS);
+        entry = bp;
+        dead = rw.failed;
+      }
+      WSTAMP(2);
+      // ---- the item's symbols
+      uint32_t bp = entry;
+      DDRun rr;
+      rr.failed = rr.at_end = false;
+      rr.t = rr.win = 0;
+      if (valid && !dead) rr = dd_run(S.T, ibe, bp, bstop, bend, sk, dctr DD_SPASS);
+      uint32_t my_exit = rr.failed ? XFAIL : bp;
+      uint32_t my_entry = dead ? XUNKNOWN : entry;
+      uint32_t c0 = sk.n;
+      WSTAMP(3);
+      // ---- verify the later items against the previous item's exit
+      for (uint32_t iter = 0; iter <= WAVE; ++iter) {
+        const uint32_t up = __shfl_up(my_exit, 1, 64);
+        const uint32_t pred = lane ? up : carry_exit;
+        const bool mism = spec && (my_entry != pred || my_entry == XUNKNOWN);
+        const uint64_t bal = __ballot(mism);
+        if (bal == 0) break;
+        DCTR(3);
+        const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
+        if (mism && !pred_mism) {
+          LdsSink s3;
+          s3.p = my_ob;
+          s3.n = 0;
+          if (pred == XFAIL || pred == XUNKNOWN || pred == DD_NONE) {
+            rr.failed = true;  // the string failed in an earlier item
+            rr.at_end = false;
+            rr.t = rr.win = 0;
+            my_exit = XFAIL;
+          } else {
+            uint32_t bq = pred;
+            rr = dd_run(S.T, ibe, bq, bstop, bend, s3, dctr DD_SPASS);
+            my_exit = rr.failed ? XFAIL : bq;
+          }
+          my_entry = pred;
+          c0 = s3.n;
+        }
+      }
+      WSTAMP(4);
+      // ---- string symbol counts: segmented scan (heads: first items)
+      const uint32_t V = valid ? c0 : 0u;
+      uint32_t ps = V;
+      int32_t hm = (!valid || k == 0) ? (int32_t)lane : -1;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o2 = __shfl_up(ps, d, 64);
+        const int32_t oh = __shfl_up(hm, d, 64);
+        if (lane >= d) {
+          ps += o2;
+          hm = max(hm, oh);
+        }
+      }
+      const uint32_t excl_h = __shfl(ps - V, hm >= 0 ? (uint32_t)hm : 0u, 64);
+      const uint32_t seg = hm >= 0 ? ps - excl_h : ps + carry_cnt;  // inclusive
+      if (valid && last)
+        dd_finish(S.T, rr.failed, rr.t, rr.win, seg,
+                  task_ovf && auto_slot(b - off0, t0 + i + 1u) > dst_cap, t0 + i, status,
+                  fstate_out, flags_out);
+      // ---- dense placement
+      const uint32_t Tinc = wave_incl_scan(V);
+      const uint32_t O_l = run + Tinc - V;
+      if (valid && k == 0) ost[i] = O_l;
+      WSTAMP(5);
+      if (V && !DD_ABL_NOSTORE) {
+        // the region in registers (one wait), then dwords realigned to the
+        // output (alignbyte), the bytes before the first aligned dword and
+        // after the last one stored singly
+        uint32_t d[DD_RB / 4 + 1];
+#pragma unroll
+        for (uint32_t w = 0; w <= DD_RB / 4; ++w) d[w] = my_ob32[w];
+        const uint64_t g0 = tbase + O_l;
+        const uint32_t h = (uint32_t)((4u - (g0 & 3u)) & 3u);  // bytes before alignment
+        const bool fits = g0 + V <= dst_cap;
+        const uint32_t nfull = V >= h ? (V - h) >> 2 : 0u;      // whole dwords
+        uint32_t vt = 0;                                         // the tail's dword
+#pragma unroll
+        for (uint32_t m = 0; m < DD_RB / 4; ++m) {
+          const uint32_t v = __builtin_amdgcn_alignbyte(d[m + 1u], d[m], h);
+          if (m < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * m) = v;
+          vt = m == nfull ? v : vt;
+        }
+        const uint32_t nh = min(h, V);
+        const uint32_t xt = h + 4u * nfull, ntl = V > xt ? V - xt : 0u;
+#pragma unroll
+        for (uint32_t x = 0; x < 3u; ++x) {
+          if (x < nh && fits) dst[g0 + x] = (uint8_t)(d[0] >> (8u * x));
+          if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
+        }
+        if (!fits) {  // near dst_cap: byte by byte, nothing at or past it
+          for (uint32_t x = 0; x < V; ++x)
+            if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
+        }
+      }
+      WSTAMP(6);
+      run += __builtin_amdgcn_readlane(Tinc, 63);
+      R0 = __builtin_amdgcn_readlane(e, nv - 1u);
+      carry_exit = __builtin_amdgcn_readlane(last ? DD_NONE : my_exit, nv - 1u);
+      carry_cnt = __builtin_amdgcn_readlane(seg, nv - 1u);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- epilogue: output starts
+    if (sl) {
+      dst_off[t0 + lane] = (uint32_t)min(tbase + ost[lane], dst_cap);
+      if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase + run, dst_cap);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  WSTAMP_FLUSH_W(DD_WAVES);
+}
+
+// ---------------------------------------------------------------------------
 // decode: the reference's nibble FSM   (lib/nghttp2_hd_huffman.c:111-143)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ src,
@@ -1535,10 +2353,10 @@ static int hip_rv(hipError_t e) {
 #if HD_DIAG_STAMPS
 extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__diag_stamps(void *out, int reset) {
   if (reset) {
-    static unsigned long long z[4096][16];
+    static unsigned long long z[4096][20];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
   }
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4096 * 16);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4096 * 20);
 }
 #endif
 
@@ -1685,7 +2503,47 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 slots
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
+  hipLaunchKernelGGL(k_decode_items,
+                     dim3(persistent_grid<k_decode_items, DD_NT, TASK_STR * DD_WAVES>(n)),
+                     dim3(DD_NT), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off, status,
+                     fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
+// The byte-balanced-piece dense decoder (pieces cross string ends), kept for
+// A/B measurement only.
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__decode_batch_pieces(const uint8_t *src,
+                                                           const uint32_t *src_off, uint32_t n,
+                                                           uint8_t *dst, size_t dst_cap,
+                                                           uint32_t *dst_off, int32_t *status,
+                                                           uint16_t *fstate, uint8_t *flags,
+                                                           void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(k_decode_dense,
+                     dim3(persistent_grid<k_decode_dense, DD_NT, TASK_STR * DD_WAVES>(n)),
+                     dim3(DD_NT), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off, status,
+                     fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
+// The round-1 engine-slot decoder (one launch, a 4-byte aligned slot of
+// auto_slot() bytes per string), kept for A/B measurement only.
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__decode_batch_slots(const uint8_t *src,
+                                                          const uint32_t *src_off, uint32_t n,
+                                                          uint8_t *dst, size_t dst_cap,
+                                                          uint32_t *dst_off, int32_t *status,
+                                                          uint16_t *fstate, uint8_t *flags,
+                                                          void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_decode<true>, dim3(persistent_grid<k_decode<true>, DEC_NT, TASK_STR * DEC_WAVES>(n)), dim3(DEC_NT), 0, st, src, src_off,
                      n, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
   return hip_rv(hipGetLastError());

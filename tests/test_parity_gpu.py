@@ -217,6 +217,28 @@ def test_full_size_config_roundtrip(codec, dev, cfg):
     assert np.array_equal(d[idx], pool[:int(off[-1])])
 
 
+def check_dense_layout(d, do, enc, eoff, tag):
+    """decode_batch_auto's layout: the strings of a task (64 consecutive
+    strings) back to back from the task's base auto_slot(x_t0, t0); string
+    i's bytes -- every byte the reference writes, the partial output of a
+    failing string included (lib/nghttp2_hd_huffman.c:122-133) -- at
+    dst[dst_off[i]:]."""
+    n = len(eoff) - 1
+    eo = eoff.astype(np.int64)
+    g = (8 * (eo - eo[0])) // 5
+    base = 4 * ((g + 3) // 4 + np.arange(n + 1))
+    for i in range(n):
+        _, out, _ = O.decode(bytes(enc[eo[i]:eo[i + 1]]), final=1)
+        w = len(out)
+        if i % 64 == 0:
+            assert do[i] == base[i], (tag, i)
+        if i + 1 < n and (i + 1) % 64:
+            assert do[i + 1] == do[i] + w, (tag, i, "not dense")
+        elif i + 1 == n:
+            assert do[n] == do[i] + w, (tag, "end")
+        assert bytes(d[do[i]:do[i] + w]) == out, (tag, i)
+
+
 def _variant_inputs():
     from nghttp2_amd import workloads as W
     pool, off, _ = W.gen_adversarial(20000, seed=31)
@@ -243,9 +265,7 @@ def test_decode_variants_match_oracle(codec, dev, variant):
             dst = torch.zeros(cap, dtype=torch.uint8, device=dev)
             dst, do, st, fs, fl = codec.decode_auto(src, so, dst=dst, want_ctx=True)
             do = do.cpu().numpy().view(np.uint32)
-            g = (8 * (eoff.astype(np.int64) - int(eoff[0]))) // 5
-            exp_do = 4 * ((g + 3) // 4 + np.arange(n + 1))
-            assert np.array_equal(do, exp_do), tag
+            check_dense_layout(dst.cpu().numpy(), do, enc, eoff, tag)
         else:
             do_t = to_dev(rdo, dev)
             dst = torch.zeros(int(rdo[-1]) + 16, dtype=torch.uint8, device=dev)
@@ -358,3 +378,37 @@ def test_emit_strings_parity(codec, dev, kind):
         off[1:] = np.cumsum([len(s) for s in strs])
         pool = np.frombuffer(b"".join(strs), dtype=np.uint8)
     check_emit(codec, dev, pool, off, kind)
+
+
+def test_dense_decode_edges(codec, dev):
+    """decode_batch_auto on strings that stress its byte-balanced pieces:
+    ends on and near piece and round boundaries, runs of empty strings (also
+    at a task's end and whole empty tasks), strings longer than a round,
+    random bytes (EOS, bad padding) -- every written byte, status and final
+    context against the oracle."""
+    import torch
+    from nghttp2_amd import workloads as W
+    rng = np.random.default_rng(0xDD)
+    parts = []
+    # encoded strings of chosen lengths (random symbols, valid padding)
+    for L in list(range(0, 70)) + [127, 128, 129, 2047, 2048, 2049, 4100, 9000]:
+        parts.append(bytes(rng.integers(0x20, 0x7F, size=max(0, L * 5 // 4), dtype=np.uint8)))
+    raw = parts + [b""] * 70 + [bytes(rng.integers(0, 256, size=int(k), dtype=np.uint8))
+                               for k in rng.integers(0, 90, size=600)]
+    raw += [b""] * 130  # whole empty tasks and empty strings at the end
+    rng.shuffle(raw[:-130])
+    lens = np.array([len(x) for x in raw], dtype=np.int64)
+    pool, off = W._pool_from_lengths(lens, np.frombuffer(b"".join(raw), np.uint8))
+    enc, eoff = O.encode_batch(pool, off)
+    garbage, goff = W.gen_all_bytes(3000, seed=77, lo=0, hi=100)
+    for tag, e, eo in (("encoded", enc, eoff), ("garbage", garbage[:int(goff[-1])], goff)):
+        rd, rdo, rst, rfs, rfl = O.decode_batch(e, eo)
+        n = len(eo) - 1
+        src = to_dev(pad16(e, eo[-1]), dev)
+        dst = torch.zeros(codec.decode_bound(int(eo[-1]), n), dtype=torch.uint8, device=dev)
+        dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eo, dev), dst=dst, want_ctx=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), rst), tag
+        assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag
+        assert np.array_equal(fl.cpu().numpy(), rfl), tag
+        check_dense_layout(dst.cpu().numpy(), do.cpu().numpy().view(np.uint32), e, eo, tag)
