@@ -216,6 +216,8 @@ struct ByteOut {
 // global output to global_* (never flat_*).
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // Word writer for encode output: the stream [o, o+E) receives big-endian
 // 32-bit groups; with phase = o & 3 fixed, each group completes one aligned
@@ -1407,6 +1409,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_BB
 #define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
 #endif
+#ifndef DD_W16
+#define DD_W16 0  // a step's two symbol bytes as one unaligned ds_write_b16
+#endif
 #define DD_NT (WAVE * DD_WAVES)
 // a lane decodes bits [8 s, 8 e + 29] at most: <= (8 P + 29) / 5 symbols,
 // plus one byte of slack (the second byte of a 1-symbol entry is written)
@@ -1425,12 +1430,23 @@ struct DDShared {
 
 // Decode symbols into a byte stream in LDS: both bytes of an entry are
 // written, the count advances by the entry's symbols.
+// k_decode_items sizes for piece bytes IP: the output region of a lane
+// (<= (8 IP + 29) / 5 symbols, one byte of slack, dword aligned), the staged
+// dwords of a wave, the staged 16-byte chunks per lane
+__host__ __device__ constexpr uint32_t di_rb(uint32_t ip) { return (((8u * ip + 29u) / 5u) + 2u + 3u) & ~3u; }
+__host__ __device__ constexpr uint32_t di_ibw(uint32_t ip) {
+  return (((WAVE * ip + DD_OV + 64u) / 4u + 8u) + 3u) & ~3u;  // whole 16-byte chunks
+}
+__host__ __device__ constexpr uint32_t di_pf(uint32_t ip) {
+  return (WAVE * ip + DD_OV + 8u + 32u + 16u * WAVE - 1u) / (16u * WAVE);
+}
+template <uint32_t IP, int IW>
 struct DIShared {  // k_decode_items
   DecTables T;  // first: the lookup at LDS offset 0
-  uint32_t ib[DD_WAVES][DD_IBW];
-  uint32_t ob[DD_WAVES][WAVE * DD_RB / 4 + 1];
-  uint32_t ostart[DD_WAVES][TASK_STR];  // string output starts (task-relative)
-  uint32_t smap[DD_WAVES][WAVE];        // a round's items -> strings (1-based, max-scanned)
+  alignas(16) uint32_t ib[IW][di_ibw(IP)];
+  uint32_t ob[IW][WAVE * di_rb(IP) / 4 + 1];
+  uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
+  uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
 };
 
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
@@ -1445,8 +1461,13 @@ struct LdsSink {
   uint32_t n;
   __device__ __forceinline__ uint32_t count() const { return n; }
   __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
-    p[n] = (uint8_t)v;
-    p[n + 1] = (uint8_t)(v >> 8);
+    if (DD_W16) {
+      const uint32_t a = (uint32_t)(uintptr_t)(p + n);
+      asm volatile("ds_write_b16 %0, %1" ::"v"(a), "v"(v));
+    } else {
+      p[n] = (uint8_t)v;
+      p[n + 1] = (uint8_t)(v >> 8);
+    }
     n += c8 >> 3;
   }
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
@@ -1798,8 +1819,9 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
       uint32_t my_exit = head ? tail_exit : (mid && !fin0 ? r0.exit : DD_NONE);
       uint32_t c0 = cnt0;
       for (uint32_t iter = 0; iter <= WAVE; ++iter) {
-        const uint32_t up = __shfl_up(my_exit, 1, 64);
-        const uint32_t pred = lane ? up : carry_exit;
+        // the previous lane's exit (wave_shr:1), lane 0 the carried one
+        const uint32_t pred = (uint32_t)__builtin_amdgcn_update_dpp(
+            (int)carry_exit, (int)my_exit, 0x138, 0xf, 0xf, false);
         const bool mism = mid && !exact0 && (r0.entry != pred || r0.entry == XUNKNOWN);
         const uint64_t bal = __ballot(mism);
         if (bal == 0) break;
@@ -1919,7 +1941,8 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restrict__ src,
+template <uint32_t IP, int IW>
+__global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
                                                         const uint32_t *__restrict__ off,
                                                         uint32_t n, uint8_t *__restrict__ dst,
                                                         uint64_t dst_cap,
@@ -1927,48 +1950,59 @@ __global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restric
                                                         int32_t *__restrict__ status,
                                                         uint16_t *__restrict__ fstate_out,
                                                         uint8_t *__restrict__ flags_out) {
-  __shared__ DIShared S;
+  __shared__ DIShared<IP, IW> S;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   lds_u32 *ibw = (lds_u32 *)S.ib[wv];
   const lds_u32 *ibe = ibw;
-  lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * DD_RB;
+  lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
   lds_u32 *ost = (lds_u32 *)S.ostart[wv];
-  stage_dec_tables(S.T, DD_NT);  // the kernel's only workgroup barrier
+  stage_dec_tables(S.T, (WAVE * IW));  // the kernel's only workgroup barrier
   WSTAMP_INIT();
   const uint32_t off0 = off[0];
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
   uint32_t dctr[4] = {0, 0, 0, 0};
   (void)dctr;
-  for (uint32_t task = blockIdx.x * DD_WAVES + wv; task < ntask; task += gridDim.x * DD_WAVES) {
+  const uint32_t tstride = gridDim.x * IW;
+  // a task's string offsets are loaded one task ahead, and the first round
+  // of the next task is staged into registers during the current task's last
+  // round (pf), so neither waits at a task start
+  uint32_t na_l = 0, nb_l = 0;
+  auto load_offs = [&](uint32_t tk) {
+    const uint32_t u0 = tk * TASK_STR;
+    const bool in = tk < ntask && lane < min(n - u0, (uint32_t)TASK_STR);
+    na_l = in ? off[u0 + lane] : 0u;
+    nb_l = in ? off[u0 + lane + 1] : 0u;
+  };
+  // the staged range of a round whose items start at byte R0 (a round's
+  // items are contiguous in the pool, the next one starting where the last
+  // one ends): [IB, IB + 16 nchunk) = [R0 - OV, min(R0 + 64 P, Z) + 8)
+  // (clipped to the task [A, Z), aligned)
+  auto round_range = [&](uint32_t R0, uint32_t A, uint32_t Z, uint32_t &IBo, uint32_t &nchunk) {
+    IBo = (R0 - A > DD_OV ? R0 - DD_OV : A) & ~15u;
+    nchunk = (((min(R0 + WAVE * IP, Z) + 8u + 15u) & ~15u) - IBo) >> 4;
+  };
+  uint4 pf[di_pf(IP)];
+  uint32_t pf_IB = 0xFFFFFFFFu;
+  load_offs(blockIdx.x * IW + wv);
+  for (uint32_t task = blockIdx.x * IW + wv; task < ntask; task += tstride) {
     WCOUNT(8);
     const uint32_t t0 = task * TASK_STR;
     const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
     const bool sl = lane < nstr;
-    const uint32_t a_l = sl ? off[t0 + lane] : 0u;
-    const uint32_t b_l = sl ? off[t0 + lane + 1] : 0u;
+    const uint32_t a_l = na_l, b_l = nb_l;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
+    load_offs(task + tstride);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
     // items: m_l of string l, X_l the first
-    const uint32_t m_l = sl ? max(1u, (b_l - a_l + DD_P - 1u) / DD_P) : 0u;
+    const uint32_t m_l = sl ? max(1u, (b_l - a_l + IP - 1u) / IP) : 0u;
     const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
     const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
-    // the staged range of a round whose items start at byte R0 (a round's
-    // items are contiguous in the pool, the next one starting where the last
-    // one ends): [IB, IB + 16 nchunk) = [R0 - OV, min(R0 + 64 P, Z) + 8)
-    // (clipped to the task, aligned)
-    auto round_range = [&](uint32_t R0, uint32_t &IBo, uint32_t &nchunk) {
-      IBo = (R0 - A > DD_OV ? R0 - DD_OV : A) & ~15u;
-      nchunk = (((min(R0 + WAVE * DD_P, Z) + 8u + 15u) & ~15u) - IBo) >> 4;
-    };
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
-    // the next round's input is loaded into registers during this round
-    uint4 pf[DD_PF];
-    uint32_t pf_IB = 0xFFFFFFFFu;
     for (uint32_t r0 = 0; r0 < M; r0 += WAVE) {
       const uint32_t nv = min(M - r0, (uint32_t)WAVE);
       const uint32_t q = r0 + lane;
@@ -1987,47 +2021,55 @@ __global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restric
       const uint32_t i = min(wave_incl_max(smap[lane]), nstr) - 1u;
       const uint32_t k = q - __shfl(X_l, i, 64);
       const uint32_t a = __shfl(a_l, i, 64), b = __shfl(b_l, i, 64);
-      const uint32_t s = a + DD_P * k, e = min(b, s + DD_P);
+      const uint32_t s = a + IP * k, e = min(b, s + IP);
       const bool last = e == b;
       const bool spec = valid && k > 0;
       WCOUNT(9);
       WSTAMP(0);
       // ---- stage [first item (- OV), last item's end + 8)
       uint32_t IB, nchunk;
-      round_range(R0, IB, nchunk);
+      round_range(R0, A, Z, IB, nchunk);
       const uint32_t IBX = IB - 16u;
       {
         const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
-        if (pf_IB != IB) {  // (the task's first round)
+        if (pf_IB != IB) {  // (not prefetched)
 #pragma unroll
-          for (uint32_t u = 0; u < DD_PF; ++u)
+          for (uint32_t u = 0; u < di_pf(IP); ++u)
             if (lane + WAVE * u < nchunk) pf[u] = g[lane + WAVE * u];
         }
 #pragma unroll
-        for (uint32_t u = 0; u < DD_PF; ++u) {
+        for (uint32_t u = 0; u < di_pf(IP); ++u) {
           const uint32_t c = lane + WAVE * u;
           if (c < nchunk) {
-            const uint32_t p = dd_phys(4u * c + 4u);
-            ibw[p] = __builtin_bswap32(pf[u].x);
-            ibw[p + 1] = __builtin_bswap32(pf[u].y);
-            ibw[p + 2] = __builtin_bswap32(pf[u].z);
-            ibw[p + 3] = __builtin_bswap32(pf[u].w);
-            if (DD_SKEW && (c & 1u) == 1u) ibw[p - 1] = __builtin_bswap32(pf[u].x);
+            u32x4 v;
+            v.x = __builtin_bswap32(pf[u].x);
+            v.y = __builtin_bswap32(pf[u].y);
+            v.z = __builtin_bswap32(pf[u].z);
+            v.w = __builtin_bswap32(pf[u].w);
+            *(lds_u32x4 *)(ibw + 4u * c + 4u) = v;
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // prefetch the next round of this task
+        // prefetch the next round: of this task, else the next task's first
         pf_IB = 0xFFFFFFFFu;
+        uint32_t IBn = 0, ncn = 0;
         if (r0 + WAVE < M) {
-          uint32_t IBn, ncn;
-          round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), IBn, ncn);
+          round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), A, Z, IBn, ncn);
+          pf_IB = IBn;
+        } else if (task + tstride < ntask) {
+          const uint32_t An = __builtin_amdgcn_readfirstlane(na_l);
+          const uint32_t Zn = __builtin_amdgcn_readlane(
+              nb_l, min(n - (task + tstride) * TASK_STR, (uint32_t)TASK_STR) - 1u);
+          round_range(An, An, Zn, IBn, ncn);
+          pf_IB = IBn;
+        }
+        if (pf_IB != 0xFFFFFFFFu) {
           const uint4 *gn = reinterpret_cast<const uint4 *>(src + IBn);
 #pragma unroll
-          for (uint32_t u = 0; u < DD_PF; ++u)
+          for (uint32_t u = 0; u < di_pf(IP); ++u)
             if (lane + WAVE * u < ncn) pf[u] = gn[lane + WAVE * u];
-          pf_IB = IBn;
         }
       }
       WSTAMP(1);
@@ -2089,57 +2131,59 @@ __global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restric
       }
       WSTAMP(4);
       // ---- string symbol counts: segmented scan (heads: first items)
+      // (the plain inclusive scan of the lanes' byte counts, less its value
+      // before the lane's last head; no head yet: plus the carried count)
       const uint32_t V = valid ? c0 : 0u;
-      uint32_t ps = V;
-      int32_t hm = (!valid || k == 0) ? (int32_t)lane : -1;
-#pragma unroll
-      for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t o2 = __shfl_up(ps, d, 64);
-        const int32_t oh = __shfl_up(hm, d, 64);
-        if (lane >= d) {
-          ps += o2;
-          hm = max(hm, oh);
-        }
-      }
-      const uint32_t excl_h = __shfl(ps - V, hm >= 0 ? (uint32_t)hm : 0u, 64);
-      const uint32_t seg = hm >= 0 ? ps - excl_h : ps + carry_cnt;  // inclusive
+      const uint32_t Tinc = wave_incl_scan(V);
+      const uint32_t h1 = wave_incl_max((!valid || k == 0) ? lane + 1u : 0u);
+      const uint32_t excl_h = __shfl(Tinc - V, h1 ? h1 - 1u : 0u, 64);
+      const uint32_t seg = h1 ? Tinc - excl_h : Tinc + carry_cnt;  // inclusive
       if (valid && last)
         dd_finish(S.T, rr.failed, rr.t, rr.win, seg,
                   task_ovf && auto_slot(b - off0, t0 + i + 1u) > dst_cap, t0 + i, status,
                   fstate_out, flags_out);
       // ---- dense placement
-      const uint32_t Tinc = wave_incl_scan(V);
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
       WSTAMP(5);
-      if (V && !DD_ABL_NOSTORE) {
-        // the region in registers (one wait), then dwords realigned to the
-        // output (alignbyte), the bytes before the first aligned dword and
-        // after the last one stored singly
-        uint32_t d[DD_RB / 4 + 1];
-#pragma unroll
-        for (uint32_t w = 0; w <= DD_RB / 4; ++w) d[w] = my_ob32[w];
+      if (!DD_ABL_NOSTORE) {
+        // dwords realigned to the output (alignbyte) for as many dwords as
+        // the wave's longest region, four per step; the bytes before the
+        // first aligned dword and after the last one stored singly
         const uint64_t g0 = tbase + O_l;
         const uint32_t h = (uint32_t)((4u - (g0 & 3u)) & 3u);  // bytes before alignment
         const bool fits = g0 + V <= dst_cap;
         const uint32_t nfull = V >= h ? (V - h) >> 2 : 0u;      // whole dwords
-        uint32_t vt = 0;                                         // the tail's dword
+        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(fits ? nfull : 0u), 63);
+        uint32_t prev = my_ob32[0];
+        const uint32_t d0 = prev;
 #pragma unroll
-        for (uint32_t m = 0; m < DD_RB / 4; ++m) {
-          const uint32_t v = __builtin_amdgcn_alignbyte(d[m + 1u], d[m], h);
-          if (m < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * m) = v;
-          vt = m == nfull ? v : vt;
-        }
-        const uint32_t nh = min(h, V);
-        const uint32_t xt = h + 4u * nfull, ntl = V > xt ? V - xt : 0u;
+        for (uint32_t m0 = 0; m0 < di_rb(IP) / 4; m0 += 4) {
+          if (m0 >= mx) break;
+          uint32_t c[4];
 #pragma unroll
-        for (uint32_t x = 0; x < 3u; ++x) {
-          if (x < nh && fits) dst[g0 + x] = (uint8_t)(d[0] >> (8u * x));
-          if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
+          for (uint32_t j = 0; j < 4; ++j) c[j] = m0 + j < di_rb(IP) / 4 ? my_ob32[m0 + j + 1u] : 0u;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t m = m0 + j;
+            const uint32_t v = __builtin_amdgcn_alignbyte(c[j], j ? c[j - 1] : prev, h);
+            if (m < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * m) = v;
+          }
+          prev = c[3];
         }
-        if (!fits) {  // near dst_cap: byte by byte, nothing at or past it
-          for (uint32_t x = 0; x < V; ++x)
-            if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
+        if (V) {
+          const uint32_t vt = __builtin_amdgcn_alignbyte(my_ob32[nfull + 1u], my_ob32[nfull], h);
+          const uint32_t nh = min(h, V);
+          const uint32_t xt = h + 4u * nfull, ntl = V > xt ? V - xt : 0u;
+#pragma unroll
+          for (uint32_t x = 0; x < 3u; ++x) {
+            if (x < nh && fits) dst[g0 + x] = (uint8_t)(d0 >> (8u * x));
+            if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
+          }
+          if (!fits) {  // near dst_cap: byte by byte, nothing at or past it
+            for (uint32_t x = 0; x < V; ++x)
+              if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
+          }
         }
       }
       WSTAMP(6);
@@ -2160,7 +2204,7 @@ __global__ __launch_bounds__(DD_NT) void k_decode_items(const uint8_t *__restric
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  WSTAMP_FLUSH_W(DD_WAVES);
+  WSTAMP_FLUSH_W(IW);
 }
 
 // ---------------------------------------------------------------------------
@@ -2360,6 +2404,45 @@ extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__diag_stamp
 }
 #endif
 
+template <uint32_t IP, int IW>
+static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
+                                uint8_t *dst, size_t dst_cap, uint32_t *dst_off,
+                                int32_t *status, uint16_t *fstate, uint8_t *flags,
+                                hipStream_t st) {
+  hipLaunchKernelGGL((k_decode_items<IP, IW>),
+                     dim3(persistent_grid<k_decode_items<IP, IW>, WAVE * IW, TASK_STR * IW>(n)),
+                     dim3(WAVE * IW), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off,
+                     status, fstate, flags);
+}
+
+// piece = 64 / 40 / 32 picks an instance; 0 picks by the batch's mean
+// encoded string length, estimated from the pool size (dst_cap is normally
+// nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 + 4 n): the strings of
+// short headers fit whole 64-byte items (no warm-up; 8 waves per CU for the
+// larger LDS regions), longer values are cut into 40-byte pieces (12 waves).
+// Every instance writes the same layout.
+static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n, uint8_t *dst,
+                        size_t dst_cap, uint32_t *dst_off, int32_t *status, uint16_t *fstate,
+                        uint8_t *flags, void *stream, int piece) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
+  if (piece == 0) {
+    const uint64_t est =
+        (uint64_t)dst_cap > 4ull * n ? ((uint64_t)dst_cap - 4ull * n) * 5u / 8u : 0u;
+    piece = est <= 48ull * n ? 64 : 40;
+  }
+  switch (piece) {
+    case 64: launch_decode_items<64u, 8>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
+    case 40: launch_decode_items<40u, 12>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
+    case 32: launch_decode_items<32u, 14>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
+    default: return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  }
+  return hip_rv(hipGetLastError());
+}
+
 extern "C" {
 
 const char *nghttp2_amd_hd_version(void) { return "nghttp2_amd_hd 0.2.0 gfx950"; }
@@ -2499,16 +2582,19 @@ int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *sr
                                           uint32_t n, uint8_t *dst, size_t dst_cap,
                                           uint32_t *dst_off, int32_t *status,
                                           uint16_t *fstate, uint8_t *flags, void *stream) {
-  hipStream_t st = (hipStream_t)stream;
-  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
-  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
-  hipLaunchKernelGGL(k_decode_items,
-                     dim3(persistent_grid<k_decode_items, DD_NT, TASK_STR * DD_WAVES>(n)),
-                     dim3(DD_NT), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off, status,
-                     fstate, flags);
-  return hip_rv(hipGetLastError());
+  return decode_items(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, stream, 0);
+}
+
+// decode_batch_auto with a chosen instance (piece bytes 64, 40 or 32), for
+// the parity tests and A/B measurement.
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__decode_batch_items(const uint8_t *src,
+                                                          const uint32_t *src_off, uint32_t n,
+                                                          uint8_t *dst, size_t dst_cap,
+                                                          uint32_t *dst_off, int32_t *status,
+                                                          uint16_t *fstate, uint8_t *flags,
+                                                          void *stream, int piece) {
+  return decode_items(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, stream,
+                      piece);
 }
 
 // The byte-balanced-piece dense decoder (pieces cross string ends), kept for

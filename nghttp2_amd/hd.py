@@ -71,6 +71,8 @@ def lib():
                                                             vp, vp]
         L.nghttp2_amd_hd_huff_decode_fsm_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp,
                                                            vp, vp, ctypes.c_int, vp]
+        L.nghttp2_amd_hd__decode_batch_items.argtypes = [vp, vp, u32, vp, sz, vp, vp, vp,
+                                                         vp, vp, ctypes.c_int]
         u64 = ctypes.c_uint64
         L.nghttp2_amd_hd_emit_strings_bound.restype = sz
         L.nghttp2_amd_hd_emit_strings_bound.argtypes = [u64, u32]
@@ -227,8 +229,11 @@ class HuffmanBatchCodec:
         return self.L.nghttp2_amd_hd_huff_decode_bound(int(enc_bytes), int(n))
 
     def decode_auto(self, src, src_off, enc_bytes=None, dst=None, dst_off=None, status=None,
-                    want_ctx=False, stream=None):
-        """Decode with engine-assigned slots (one launch).  Returns
+                    want_ctx=False, stream=None, piece=0):
+        """Decode into a dense pool (one launch): the strings of each task of
+        64 consecutive strings back to back from the task's base
+        auto_slot(x_t0, t0).  piece = 64 / 40 / 32 forces an instance of the
+        item decoder (tests, A/B); 0 lets the library pick.  Returns
         (dst, dst_off, status[, fstate, flags])."""
         torch = self.torch
         n = src_off.numel() - 1
@@ -245,9 +250,12 @@ class HuffmanBatchCodec:
         if want_ctx:
             fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
             flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
-        rv = self.L.nghttp2_amd_hd_huff_decode_batch_auto(
-            _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(status),
-            _p(fstate), _p(flags), _stream(stream))
+        args = (_p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(status),
+                _p(fstate), _p(flags), _stream(stream))
+        if piece:
+            rv = self.L.nghttp2_amd_hd__decode_batch_items(*args, piece)
+        else:
+            rv = self.L.nghttp2_amd_hd_huff_decode_batch_auto(*args)
         _check(rv, "decode_batch_auto")
         if want_ctx:
             return dst, dst_off, status[:n], fstate[:n], flags[:n]

@@ -250,20 +250,22 @@ def _variant_inputs():
     yield "mixed", e3, eo3
 
 
-@pytest.mark.parametrize("variant", ["auto", "fsm"])
+@pytest.mark.parametrize("variant", ["auto", "items64", "items40", "items32", "fsm"])
 def test_decode_variants_match_oracle(codec, dev, variant):
-    """decode_batch_auto (engine slots) and the batched reference FSM kernel
-    agree with the oracle on status, final context and every written byte."""
+    """decode_batch_auto (dense item decoder: the library's pick and every
+    instance) and the batched reference FSM kernel agree with the oracle on
+    status, final context and every written byte."""
     import torch
     for tag, enc, eoff in _variant_inputs():
         rd, rdo, rst, rfs, rfl = O.decode_batch(enc, eoff)
         src = to_dev(pad16(enc, eoff[-1]), dev)
         so = to_dev(eoff, dev)
         n = len(eoff) - 1
-        if variant == "auto":
+        if variant != "fsm":
             cap = codec.decode_bound(int(eoff[-1]), n)
             dst = torch.zeros(cap, dtype=torch.uint8, device=dev)
-            dst, do, st, fs, fl = codec.decode_auto(src, so, dst=dst, want_ctx=True)
+            piece = 0 if variant == "auto" else int(variant[5:])
+            dst, do, st, fs, fl = codec.decode_auto(src, so, dst=dst, want_ctx=True, piece=piece)
             do = do.cpu().numpy().view(np.uint32)
             check_dense_layout(dst.cpu().numpy(), do, enc, eoff, tag)
         else:
@@ -380,8 +382,10 @@ def test_emit_strings_parity(codec, dev, kind):
     check_emit(codec, dev, pool, off, kind)
 
 
-def test_dense_decode_edges(codec, dev):
-    """decode_batch_auto on strings that stress its byte-balanced pieces:
+@pytest.mark.parametrize("piece", [0, 64, 40, 32])
+def test_dense_decode_edges(codec, dev, piece):
+    """decode_batch_auto (each item-decoder instance) on strings that stress
+    its pieces:
     ends on and near piece and round boundaries, runs of empty strings (also
     at a task's end and whole empty tasks), strings longer than a round,
     random bytes (EOS, bad padding) -- every written byte, status and final
@@ -406,7 +410,8 @@ def test_dense_decode_edges(codec, dev):
         n = len(eo) - 1
         src = to_dev(pad16(e, eo[-1]), dev)
         dst = torch.zeros(codec.decode_bound(int(eo[-1]), n), dtype=torch.uint8, device=dev)
-        dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eo, dev), dst=dst, want_ctx=True)
+        dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eo, dev), dst=dst, want_ctx=True,
+                                                piece=piece)
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), rst), tag
         assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag

@@ -31,9 +31,12 @@ def main():
     L0 = hd.lib()
     L0.nghttp2_amd_hd__decode_batch_slots.argtypes = ARGS
     L0.nghttp2_amd_hd__decode_batch_pieces.argtypes = ARGS
+    L0.nghttp2_amd_hd__decode_batch_items.argtypes = ARGS + [ctypes.c_int]
     kern = {"dense": L0.nghttp2_amd_hd_huff_decode_batch_auto,
             "slots_r1": L0.nghttp2_amd_hd__decode_batch_slots,
             "pieces": L0.nghttp2_amd_hd__decode_batch_pieces}
+    for pc in (64, 40, 32):
+        kern["items%d" % pc] = (lambda pc: lambda *a: L0.nghttp2_amd_hd__decode_batch_items(*a, pc))(pc)
     for p in sorted(glob.glob(os.path.join(HERE, "lib_*.so"))):
         kern[os.path.basename(p)[4:-3]] = load(p).nghttp2_amd_hd_huff_decode_batch_auto
     out = {}
