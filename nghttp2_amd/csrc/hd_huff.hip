@@ -409,7 +409,7 @@ __device__ __host__ __forceinline__ uint64_t enc_piece_slot(uint32_t rel, uint32
   return (uint64_t)(rel / ENC_PIECE) + s + k;
 }
 
-__global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(WG) void k_enc_count_r1(const uint8_t *__restrict__ src,
                                                   const uint32_t *__restrict__ off,
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
 // ---------------------------------------------------------------------------
 #define ENC_RW 1024u  // LDS words per wave image: 1 KB of input at <= 30 bits a byte + edges
 
-__global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(WG) void k_encode_r1(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
@@ -697,6 +697,319 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
     __builtin_amdgcn_wave_barrier();
     Pc += __builtin_amdgcn_readlane(Sinc, 63);
     scarry = max(__builtin_amdgcn_readlane(sm, 63), cd[64]);
+    x = xe;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// encode over aligned chunks (the product path): a wave owns 64 consecutive
+// strings, i.e. the contiguous raw bytes [A, Z), and walks them as aligned
+// 16-byte chunks, 64 per round (one per lane), whatever the string lengths.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// Pass 1 (lib/nghttp2_hd_huffman.c:34-43): code bits per string.  With P(x)
+// = the code bits of the wave's bytes from its first chunk up to byte x, a
+// string's bits are P(b) - P(a): each lane sums its chunk's code lengths
+// (in-chunk exclusive prefixes to LDS, 16 bits a byte), a wave scan places
+// the chunks, and every string lane reads P at its two ends.  Bytes before
+// A or past Z in the edge chunks add the same amount to both ends.
+__global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
+                                                  const uint32_t *__restrict__ off,
+                                                  uint32_t n,
+                                                  uint32_t *__restrict__ out_len,
+                                                  uint32_t *__restrict__ tile_sums,
+                                                  int bits_out) {
+  __shared__ uint8_t lenT[256];
+  __shared__ alignas(16) uint32_t pre[ENC_WAVES][512];  // a round's prefixes (u16 per byte)
+  __shared__ uint32_t red[WG / 64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;  // the wave's strings
+  uint32_t e = 0;
+  if (t0 < n) {
+    const uint32_t nstr = min(n - t0, 64u);
+    const bool sl = lane < nstr;
+    const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+    const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+    const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
+    const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
+    lds_u32 *pr = (lds_u32 *)pre[wv];
+    const lds_u16 *pr16 = (const lds_u16 *)pre[wv];
+    uint32_t Rc = 0, Pa = 0, Pb = 0;
+    bool ga = false, gb = false;
+    uint4 wn = make_uint4(0, 0, 0, 0);
+    if (c0 + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + ((c0 + lane) << 4));
+    for (uint32_t cb = c0; cb < c_end; cb += 64u) {
+      const uint32_t base = cb << 4;
+      const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
+      wn = make_uint4(0, 0, 0, 0);
+      if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + base + 1024u + 16u * lane);
+      uint32_t run = 0, pk[8];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t L = lenT[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+        if (j & 1) pk[j >> 1] |= run << 16; else pk[j >> 1] = run;
+        run += L;
+      }
+      u32x4 v0, v1;
+      v0.x = pk[0]; v0.y = pk[1]; v0.z = pk[2]; v0.w = pk[3];
+      v1.x = pk[4]; v1.y = pk[5]; v1.z = pk[6]; v1.w = pk[7];
+      *(lds_u32x4 *)(pr + 8u * lane) = v0;
+      *(lds_u32x4 *)(pr + 8u * lane + 4u) = v1;
+      const uint32_t Sinc = wave_incl_scan(run), Sx = Sinc - run;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the string ends in this round: P = chunk start + in-chunk prefix
+      const uint32_t ra = a_l - base, rb = b_l - base;
+      const uint32_t xa = __shfl(Sx, (ra >> 4) & 63u, 64), xb = __shfl(Sx, (rb >> 4) & 63u, 64);
+      if (sl && ra < 1024u) {
+        Pa = Rc + xa + pr16[ra];
+        ga = true;
+      }
+      if (sl && rb < 1024u) {
+        Pb = Rc + xb + pr16[rb];
+        gb = true;
+      }
+      Rc += __builtin_amdgcn_readlane(Sinc, 63);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // an end at the last chunk's end (Z on a chunk boundary)
+    if (!ga) Pa = Rc;
+    if (!gb) Pb = Rc;
+    const uint32_t bits = sl ? Pb - Pa : 0u;
+    e = (bits + 7u) >> 3;
+    if (sl && out_len) out_len[t0 + lane] = bits_out ? bits : e;
+  }
+  if (tile_sums) {
+    uint32_t tot;
+    block_excl_scan<WG>(e, red, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+  }
+}
+
+// Pass 2 (lib/nghttp2_hd_huffman.c:45-104): bit packing.  The EOS-prefix
+// padding of a string (:95-101, pad = 8 E - bits, known from pass 1) is
+// counted as extra length of its last byte's code (codes are MSB-aligned, so
+// the pad is just zero bits after the code), so the bit stream of the wave
+// is the plain concatenation of every byte's code and every string's pad,
+// and a chunk starts at the wave scan of the chunk lengths -- no per-byte
+// alignment.  A lane combines its 16 codes in registers (pairs of < 32
+// bits, then quads of < 64) and ORs each quad into the round's LDS image
+// (three words); a round with a longer pair goes byte by byte.  The pad
+// bits themselves are all ones, OR'ed in by the string's own lane.  The
+// image goes out as whole big-endian dwords (the dwords at the wave's two
+// ends bytewise), the partial last word carried into the next round.  The
+// first chunk's bytes before A are placed before the wave's first bit, in
+// a margin of the image that is never stored.
+#define EC_M 16u                    // image margin (words): >= 15 bytes x 30 bits
+#define EC_RW (EC_M + 1024u + 32u)  // + 1 KB at <= 32 bits a byte + carry + bytes past Z
+
+// OR the MSB-aligned bits {hi, lo} into the image at bit b
+__device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, uint32_t lo) {
+  const uint32_t o = b & 31u;
+  lds_u32 *q = img + (b >> 5);
+  atomicOr((uint32_t *)&q[0], hi >> o);
+  atomicOr((uint32_t *)&q[1], __builtin_amdgcn_alignbit(hi, lo, o));
+  atomicOr((uint32_t *)&q[2], __builtin_amdgcn_alignbit(lo, 0u, o));  // (0 when o = 0)
+}
+
+__global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
+                                               const uint32_t *__restrict__ off, uint32_t n,
+                                               uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                               uint32_t *__restrict__ dst_off,
+                                               const uint32_t *__restrict__ tile_sums) {
+  __shared__ uint2 codeT[256];  // {code MSB-aligned, length}
+  __shared__ uint32_t image[ENC_WAVES][EC_RW];
+  __shared__ alignas(16) uint32_t padb[ENC_WAVES][256];  // a round's pad bits (u8 per byte)
+  __shared__ uint32_t o_sh[WG + 1];
+  __shared__ uint32_t red[2 * (WG / 64)];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
+  lds_u32 *img = (lds_u32 *)image[wv];
+  for (uint32_t i = lane; i < EC_RW; i += 64u) img[i] = 0u;
+  lds_u32 *pdw = (lds_u32 *)padb[wv];
+  lds_u8 *pdb = (lds_u8 *)padb[wv];
+#pragma unroll
+  for (uint32_t i = 0; i < 4u; ++i) pdw[lane + 64u * i] = 0u;
+  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
+  const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
+  const uint32_t E_me = (bits_me + 7u) >> 3;
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
+  const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
+  const bool sl = lane < nstr;
+  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+  const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+  const uint32_t Z = nstr ? __builtin_amdgcn_readlane(b_l, nstr - 1u) : 0u;
+  const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
+  uint4 wn = make_uint4(0, 0, 0, 0);  // the next round's chunk (prefetched)
+  if (c0 + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + ((c0 + lane) << 4));
+  // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
+  // strings, L2-resident), summed with independent loads in flight, in 64
+  // bits (a batch's encoded total may pass the uint32 offset range)
+  uint64_t pre = 0;
+  {
+    uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t t = threadIdx.x;
+    for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p8[k] += tile_sums[t + k * WG];
+    }
+    for (; t < blockIdx.x; t += WG) pre += tile_sums[t];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pre += p8[k];
+  }
+  uint32_t tot, ptot_lo, ptot_hi;
+  // the 64-bit prefix as two 32-bit sums: 256 parts of 23 bits fit 31 bits
+  const uint32_t loc = block_excl_scan_sum<WG>(E_me, (uint32_t)(pre & 0x7FFFFFu), red, &tot,
+                                               &ptot_lo);  // (barriers)
+  {
+    uint32_t dummy;
+    block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
+  }
+  const uint64_t ptot = ((uint64_t)ptot_hi << 23) + ptot_lo;
+  // uint32 offsets: a tile whose strings would end past the limit writes no
+  // bytes, saturated offsets and the overflow mark in dst_off[n]
+  const uint64_t limit = dst_cap < 0xFFFFFFFEull ? dst_cap : 0xFFFFFFFEull;
+  if (ptot + tot > limit) {
+    if (s_me < n) dst_off[s_me] = (uint32_t)min(ptot + loc, limit);
+    if (s_me == n - 1u) dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW;
+    return;
+  }
+  const uint32_t o_me = (uint32_t)ptot + loc;
+  if (s_me < n) dst_off[s_me] = o_me;
+  if (s_me == n - 1u) dst_off[n] = o_me + E_me;
+  o_sh[threadIdx.x] = o_me;
+  if (threadIdx.x == WG - 1) o_sh[WG] = o_me + E_me;
+  __syncthreads();
+  if (nstr == 0) return;
+  const uint32_t OA = o_sh[64u * wv], OZ = o_sh[64u * wv + nstr];  // the wave's output bytes
+  const uint64_t G0 = 8ull * OA;
+  const uint32_t pad_l = sl ? 8u * E_me - bits_me : 0u;  // EOS-prefix bits after string l
+  const uint32_t olast_l = o_me + E_me - 1u;             // its last output byte (if E > 0)
+  const uint32_t tail_l = b_l - 1u;                      // its last raw byte
+  uint32_t x = 0;  // output bit of the round's first wave byte (relative to G0)
+  for (uint32_t cb = c0; cb < c_end; cb += 64u) {
+    const bool first = cb == c0, last_round = cb + 64u >= c_end;
+    const uint32_t base = cb << 4;
+    const uint64_t WB = (G0 + x) >> 5;  // global word of img[EC_M]
+    // ---- pads of the strings ending in this round, at their last raw byte
+    const bool tl = sl && pad_l && b_l > a_l && tail_l - base < 1024u;
+    if (tl) pdb[tail_l - base] = (uint8_t)pad_l;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t p0 = base + 16u * lane;
+    const bool act = p0 < Z;  // (lanes past the wave's last chunk: nothing)
+    const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
+    wn = make_uint4(0, 0, 0, 0);
+    if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + p0 + 1024u);
+    const u32x4 pdv = *(const lds_u32x4 *)(pdw + 4u * lane);
+    const uint32_t pd[4] = {pdv.x, pdv.y, pdv.z, pdv.w};
+    uint32_t c[16], l[16];
+#define EC_B8(j) (((j) & 3) ? (wd[(j) >> 2] >> (8 * ((j) & 3) - 3)) & 0x7F8u : (wd[(j) >> 2] << 3) & 0x7F8u)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(j));
+      c[j] = cj.x;
+      l[j] = cj.y + ((pd[j >> 2] >> (8 * (j & 3))) & 0xFFu);  // (+ the pad at a string's last byte)
+    }
+    // pairs {pc, pl}: MSB-aligned, < 32 bits; quads {qh, ql}: < 64 bits
+    uint32_t pc[8], pl[8], plx = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pl[k] = l[2 * k] + l[2 * k + 1];
+      pc[k] = c[2 * k] | (c[2 * k + 1] >> l[2 * k]);
+      plx = max(plx, pl[k]);
+    }
+    uint32_t qh[4], qo[4], ql[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      ql[m] = pl[2 * m] + pl[2 * m + 1];
+      qh[m] = pc[2 * m] | (pc[2 * m + 1] >> pl[2 * m]);
+      qo[m] = __builtin_amdgcn_alignbit(pc[2 * m + 1], 0u, pl[2 * m]);
+    }
+    const uint32_t S = act ? ql[0] + ql[1] + ql[2] + ql[3] : 0u;
+    const bool longp = __ballot(act && plx > 31u) != 0;  // a pair of 32 bits or more: bytewise
+    // ---- the first chunk's bytes before A go before the wave's first bit
+    uint32_t RA = 0;
+    if (first) {
+      const uint32_t k = A & 15u;
+      uint32_t ra = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ra += (uint32_t)j < k ? l[j] : 0u;
+      RA = __builtin_amdgcn_readfirstlane(ra);
+    }
+    const uint32_t Sinc = wave_incl_scan(S);
+    // my chunk's first bit in the image (img[0] = global word WB - EC_M)
+    const uint32_t ib0 = (uint32_t)(G0 + x - 32ull * WB) + 32u * EC_M + (Sinc - S) - RA;
+    if (act) {
+      if (!longp) {
+        uint32_t b = ib0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          ec_or3(img, b, qh[m], qo[m]);
+          b += ql[m];
+        }
+      } else {
+        uint32_t b = ib0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {  // a code of <= 37 bits, MSB-aligned in 64
+          const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(j));
+          const uint32_t lj = cj.y + ((pd[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+          ec_or3(img, b, cj.x, 0u);
+          b += lj;
+        }
+      }
+    }
+#undef EC_B8
+    // ---- EOS-prefix padding (all ones) of the strings that end in this round
+    if (tl) {
+      const uint32_t r = (uint32_t)((olast_l >> 2) - WB) + EC_M;
+      atomicOr((uint32_t *)&img[r], ((1u << pad_l) - 1u) << (24u - 8u * (olast_l & 3u)));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- store whole words and zero them; carry a partial last word
+    const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) - RA;
+    const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
+    const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
+    for (uint32_t i = lane; i < nst; i += 64u) {
+      const uint32_t v = __builtin_bswap32(img[EC_M + i]);
+      img[EC_M + i] = 0u;
+      const uint64_t ga = 4ull * (WB + i);
+      if (ga >= OA && ga + 4u <= OZ && ga + 4u <= dst_cap) {
+        *reinterpret_cast<uint32_t *>(dst + ga) = v;
+      } else {
+        for (uint32_t y = 0; y < 4u; ++y) {
+          const uint64_t gq = ga + y;
+          if (gq >= OA && gq < OZ && gq < dst_cap) dst[gq] = (uint8_t)(v >> (8u * y));
+        }
+      }
+    }
+    if (first && lane < EC_M) img[lane] = 0u;  // the bytes before A
+    if (tl) pdb[tail_l - base] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!last_round && nst < nw) {  // the partial word moves to img[EC_M]
+      const uint32_t cw = img[EC_M + nst];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane == 0) {
+        img[EC_M + nst] = 0u;
+        img[EC_M] = cw;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     x = xe;
   }
 }
@@ -2483,7 +2796,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
-                     src_off, n, enc_len, (uint32_t *)nullptr, (uint16_t *)nullptr, 0);
+                     src_off, n, enc_len, (uint32_t *)nullptr, 0);
   return hip_rv(hipGetLastError());
 }
 
@@ -2499,9 +2812,29 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles,
-                     (uint16_t *)nullptr, 1);
+  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
   hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+  return hip_rv(hipGetLastError());
+}
+
+// The round-1 encode kernels (byte-aligned heads inside chunks), kept for
+// A/B measurement only.
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__encode_batch_r1(const uint8_t *src, const uint32_t *src_off,
+                                                       uint32_t n, uint8_t *dst, size_t dst_cap,
+                                                       uint32_t *dst_off, void *workspace,
+                                                       size_t workspace_size, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !workspace) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (workspace_size < nghttp2_amd_hd_huff_workspace_size(n))
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  const uint32_t nt = ntiles_for(n);
+  uint32_t *tiles = (uint32_t *)workspace;
+  hipLaunchKernelGGL(k_enc_count_r1, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles,
+                     (uint16_t *)nullptr, 1);
+  hipLaunchKernelGGL(k_encode_r1, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
 }
