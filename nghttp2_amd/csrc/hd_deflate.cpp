@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -132,7 +133,17 @@ struct Engine {
   uint8_t *d_in = nullptr, *d_out = nullptr, *d_ws = nullptr;
   uint32_t *d_off = nullptr;
   size_t din_cap = 0, dout_cap = 0, dws_cap = 0, doff_cap = 0;
+  uint32_t *h_nt = nullptr, *d_nt = nullptr;  // name tokens and hashes
+  size_t hnt_cap = 0, dnt_cap = 0;
 };
+// Batches of at least this many field names take their tokens and hashes
+// from one k_name_tokens launch (NGHTTP2_AMD_GPU_NAMES_MIN; 0 = always);
+// smaller ones from the host lookup, which costs less than a GPU round trip.
+std::atomic<uint32_t> g_names_min{[] {
+  const char *e = getenv("NGHTTP2_AMD_GPU_NAMES_MIN");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : 2048u;
+}()};
+uint32_t gpu_names_min() { return g_names_min.load(); }
 Engine &engine() {
   static Engine e;
   return e;
@@ -183,6 +194,8 @@ struct Piece {
 extern "C" {
 
 NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__test_fail_deflate_gpu(int n) { g_fail_gpu.store(n); }
+// (tests, A/B) the batch size from which field names go through the GPU
+NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__set_gpu_names_min(uint32_t n) { g_names_min.store(n); }
 
 int nghttp2_amd_hd_deflate_new(nghttp2_amd_hd_deflater **deflater_ptr,
                                size_t max_deflate_dynamic_table_size) {
@@ -270,10 +283,50 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   for (uint32_t i = 0; i < nblocks; ++i)
     if (!deflaters[i] || block_nv_off[i] > block_nv_off[i + 1]) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
 
-  // ---- pass 1: representations; one task per connection, its lists in
-  // batch order (connections are independent)
   using nghttp2_amd_host::parallel_for;
   nghttp2_amd_host::Phases ph("deflate");
+  // ---- the token and hash of every field name of the batch (lookup_token,
+  // name_hash; deflate_nv, lib/nghttp2_hd.c:1388-1393): one GPU launch over
+  // the batch's names, before any deflater changes (a failure here leaves
+  // the deflaters as they were)
+  const uint32_t f0 = block_nv_off[0], nf = block_nv_off[nblocks] - f0;
+  std::vector<uint32_t> fnt;  // hash[nf], then token[nf]
+  if (nf && nf >= gpu_names_min()) {
+    std::vector<uint64_t> nbase(nf + 1, 0);
+    for (uint32_t k = 0; k < nf; ++k) nbase[k + 1] = nbase[k] + nva[f0 + k].namelen;
+    const uint64_t nraw = nbase[nf];
+    if (nraw > UINT32_MAX) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+    const size_t in_bytes = ((size_t)nraw + 15u) / 16u * 16u + 16u;
+    std::lock_guard<std::mutex> guard(engine().mu);
+    Engine &E = engine();
+    hipStream_t st = (hipStream_t)stream;
+    if (!grow_host((void **)&E.h_in, &E.hin_cap, in_bytes) ||
+        !grow_host((void **)&E.h_off, &E.hoff_cap, ((size_t)nf + 1u) * sizeof(uint32_t)) ||
+        !grow_host((void **)&E.h_nt, &E.hnt_cap, 2u * (size_t)nf * sizeof(uint32_t)) ||
+        !grow_dev((void **)&E.d_in, &E.din_cap, in_bytes) ||
+        !grow_dev((void **)&E.d_off, &E.doff_cap, ((size_t)nf + 1u) * sizeof(uint32_t)) ||
+        !grow_dev((void **)&E.d_nt, &E.dnt_cap, 2u * (size_t)nf * sizeof(uint32_t)))
+      return NGHTTP2_AMD_ERR_NOMEM;
+    parallel_for(nf, 4096, [&](size_t k) {
+      E.h_off[k] = (uint32_t)nbase[k];
+      if (nva[f0 + k].namelen) memcpy(E.h_in + nbase[k], nva[f0 + k].name, nva[f0 + k].namelen);
+    });
+    E.h_off[nf] = (uint32_t)nraw;
+    memset(E.h_in + nraw, 0, in_bytes - nraw);
+    if (fault_inject_gpu() ||
+        !hip_ok(hipMemcpyAsync(E.d_in, E.h_in, in_bytes, hipMemcpyHostToDevice, st), "H2D") ||
+        !hip_ok(hipMemcpyAsync(E.d_off, E.h_off, ((size_t)nf + 1u) * sizeof(uint32_t), hipMemcpyHostToDevice, st), "H2D"))
+      return NGHTTP2_AMD_ERR_FATAL;
+    int rv = nghttp2_amd_hd_name_tokens_batch(E.d_in, E.d_off, nf, (int32_t *)(E.d_nt + nf), E.d_nt, stream);
+    if (rv) return rv;
+    if (!hip_ok(hipMemcpyAsync(E.h_nt, E.d_nt, 2u * (size_t)nf * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "D2H") ||
+        !hip_ok(hipStreamSynchronize(st), "sync"))
+      return NGHTTP2_AMD_ERR_FATAL;
+    fnt.assign(E.h_nt, E.h_nt + 2u * (size_t)nf);
+    ph.mark("names");
+  }
+  // ---- pass 1: representations; one task per connection, its lists in
+  // batch order (connections are independent)
   std::vector<std::vector<Piece>> pieces(nblocks);
   std::vector<std::vector<std::pair<const uint8_t *, uint32_t>>> blits(nblocks);
   auto deflate_list = [&](uint32_t i) {
@@ -300,8 +353,9 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     }
     for (uint32_t k = block_nv_off[i]; k < block_nv_off[i + 1]; ++k) {
       const nghttp2_amd_nv &nv = nva[k];
-      const uint32_t nh = name_hash(nv.name, nv.namelen);
-      const int32_t token = hdtok::lookup_token(nv.name, nv.namelen, nh);
+      const uint32_t nh = fnt.empty() ? name_hash(nv.name, nv.namelen) : fnt[k - f0];
+      const int32_t token = fnt.empty() ? hdtok::lookup_token(nv.name, nv.namelen, nh)
+                                        : (int32_t)fnt[nf + (k - f0)];
       const size_t room = nv.namelen + nv.valuelen + kEntryOverhead;
       // deflate_nv (:1373-1400): never-index authorization, short cookies
       // and fields flagged NO_INDEX; hd_deflate_decide_indexing (:1358-1371)

@@ -739,13 +739,16 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     const lds_u16 *pr16 = (const lds_u16 *)pre[wv];
     uint32_t Rc = 0, Pa = 0, Pb = 0;
     bool ga = false, gb = false;
-    uint4 wn = make_uint4(0, 0, 0, 0);
+    // chunks are loaded two rounds ahead (enough bytes in flight per CU)
+    uint4 wn = make_uint4(0, 0, 0, 0), wn2 = make_uint4(0, 0, 0, 0);
     if (c0 + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + ((c0 + lane) << 4));
+    if (c0 + 64u + lane < c_end) wn2 = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u + lane) << 4));
     for (uint32_t cb = c0; cb < c_end; cb += 64u) {
       const uint32_t base = cb << 4;
       const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
-      wn = make_uint4(0, 0, 0, 0);
-      if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + base + 1024u + 16u * lane);
+      wn = wn2;
+      wn2 = make_uint4(0, 0, 0, 0);
+      if (cb + 128u + lane < c_end) wn2 = *reinterpret_cast<const uint4 *>(src + base + 2048u + 16u * lane);
       uint32_t run = 0, pk[8];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -806,6 +809,9 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
+#ifndef EC_WPE
+#define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
+#endif
 #define EC_M 16u                    // image margin (words): >= 15 bytes x 30 bits
 #define EC_RW (EC_M + 1024u + 32u)  // + 1 KB at <= 32 bits a byte + carry + bytes past Z
 
@@ -818,7 +824,7 @@ __device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, ui
   atomicOr((uint32_t *)&q[2], __builtin_amdgcn_alignbit(lo, 0u, o));  // (0 when o = 0)
 }
 
-__global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
@@ -979,16 +985,21 @@ __global__ __launch_bounds__(WG) void k_encode(const uint8_t *__restrict__ src,
     const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) - RA;
     const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
     const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
+    // words [ilo, ihi) lie inside the wave's output [OA, OZ) (<= dst_cap by
+    // the tile check); the others hold bytes of the neighbouring waves
+    const uint32_t ilo = (uint32_t)(((uint64_t)OA + 3u) / 4u - min(WB, ((uint64_t)OA + 3u) / 4u));
+    const uint32_t ihi = (uint32_t)((uint64_t)OZ / 4u > WB ? (uint64_t)OZ / 4u - WB : 0u);
+    uint8_t *const dw = dst + 4ull * WB;  // (uniform)
     for (uint32_t i = lane; i < nst; i += 64u) {
       const uint32_t v = __builtin_bswap32(img[EC_M + i]);
       img[EC_M + i] = 0u;
-      const uint64_t ga = 4ull * (WB + i);
-      if (ga >= OA && ga + 4u <= OZ && ga + 4u <= dst_cap) {
-        *reinterpret_cast<uint32_t *>(dst + ga) = v;
+      if (i >= ilo && i < ihi) {
+        *reinterpret_cast<uint32_t *>(dw + 4u * i) = v;
       } else {
+        const uint64_t ga = 4ull * (WB + i);
         for (uint32_t y = 0; y < 4u; ++y) {
           const uint64_t gq = ga + y;
-          if (gq >= OA && gq < OZ && gq < dst_cap) dst[gq] = (uint8_t)(v >> (8u * y));
+          if (gq >= OA && gq < OZ) dst[gq] = (uint8_t)(v >> (8u * y));
         }
       }
     }

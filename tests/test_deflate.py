@@ -127,9 +127,30 @@ def test_rfc7541_c4_product():
     assert [x.hex() for x in w] == [b["wire"] for b in ex["blocks"]]
 
 
+def _names_min(n):
+    import ctypes
+    from nghttp2_amd import hd
+    L = hd._deflate_lib()
+    L.nghttp2_amd_hd__set_gpu_names_min.argtypes = [ctypes.c_uint32]
+    L.nghttp2_amd_hd__set_gpu_names_min.restype = None
+    L.nghttp2_amd_hd__set_gpu_names_min(n)
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("names", ["host", "gpu"])
 @pytest.mark.parametrize("table", [4096, 256, 0])
-def test_deflate_random_connections_vs_oracle_and_roundtrip(table):
+def test_deflate_random_connections_vs_oracle_and_roundtrip(table, names):
+    """names: the field names' tokens and hashes from the host lookup, or
+    from one k_name_tokens launch over the batch (the large-batch path)."""
+    import nghttp2_amd
+    _names_min(0 if names == "gpu" else 1 << 30)
+    try:
+        _deflate_random(table)
+    finally:
+        _names_min(2048)
+
+
+def _deflate_random(table):
     import nghttp2_amd
     rng = np.random.Generator(np.random.PCG64(0xDEF1 + table))
     nconn, rounds = 10, 6
@@ -213,3 +234,26 @@ def test_deflate_gpu_stage_failure_turns_deflaters_bad_cpu():
     for d in (d1, d2):
         st, w = nghttp2_amd.deflate_blocks([d], [[(b":method", b"GET")]])
         assert st[0] == hd.NGHTTP2_ERR_HEADER_COMP and w[0] == b""
+
+
+def test_deflate_names_stage_failure_leaves_deflaters_cpu():
+    """The batched name lookup runs before pass 1: a failure there returns
+    the error and leaves every deflater as it was (not bad)."""
+    import ctypes
+    import nghttp2_amd
+    from nghttp2_amd import hd
+    L = hd._deflate_lib()
+    L.nghttp2_amd_hd__test_fail_deflate_gpu.argtypes = [ctypes.c_int]
+    L.nghttp2_amd_hd__test_fail_deflate_gpu.restype = None
+    d = nghttp2_amd.HpackDeflater()
+    _names_min(0)
+    L.nghttp2_amd_hd__test_fail_deflate_gpu(1)
+    try:
+        with pytest.raises(RuntimeError):
+            nghttp2_amd.deflate_blocks([d], [[(b"x-custom", b"value-one")]])
+    finally:
+        L.nghttp2_amd_hd__test_fail_deflate_gpu(0)
+        _names_min(2048)
+    assert d.dynamic_table() == []
+    st, w = nghttp2_amd.deflate_blocks([d], [[(b":method", b"GET")]])
+    assert st[0] == 1 and w[0] == b"\x82"

@@ -3,7 +3,7 @@
 interleaved: the product's nghttp2_amd_hd_huff_encode_batch against the
 round-1 kernels (nghttp2_amd_hd__encode_batch_r1).  Outputs are checked
 equal.  Usage: ab_encode.py [config 2|3|9 ...]  (9 = all byte values)"""
-import ctypes, json, os, sys
+import ctypes, glob, json, os, sys
 import numpy as np
 import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -21,6 +21,10 @@ def main():
     L = hd.lib()
     L.nghttp2_amd_hd__encode_batch_r1.argtypes = ARGS
     kern = {"product": L.nghttp2_amd_hd_huff_encode_batch, "r1": L.nghttp2_amd_hd__encode_batch_r1}
+    for p in sorted(glob.glob(os.path.join(HERE, "lib_*.so"))):  # tools/diag variant builds
+        Lv = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+        Lv.nghttp2_amd_hd_huff_encode_batch.argtypes = ARGS
+        kern[os.path.basename(p)[4:-3]] = Lv.nghttp2_amd_hd_huff_encode_batch
     for cfg in cfgs:
         if cfg == 9:
             pool, off = W.gen_all_bytes(1 << 18)
@@ -47,10 +51,12 @@ def main():
             for _ in range(3):
                 run(k)
         torch.cuda.synchronize()
-        a, b = bufs["product"], bufs["r1"]
-        assert torch.equal(a[1], b[1]), "offsets differ"
+        a = bufs["product"]
         E = int(a[1][-1].item())
-        assert torch.equal(a[0][:E], b[0][:E]), "bytes differ"
+        for k in kern:
+            b = bufs[k]
+            assert torch.equal(a[1], b[1]), k + ": offsets differ"
+            assert torch.equal(a[0][:E], b[0][:E]), k + ": bytes differ"
         res = {k: [] for k in kern}
         for _ in range(10):
             for k in kern:
