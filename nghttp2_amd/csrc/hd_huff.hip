@@ -809,6 +809,9 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
+#ifndef EC_SB
+#define EC_SB 0  // k_encode: a scheduling barrier after every two dwords of lookups
+#endif
 #ifndef EC_WPE
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
 #endif
@@ -916,38 +919,38 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + p0 + 1024u);
     const u32x4 pdv = *(const lds_u32x4 *)(pdw + 4u * lane);
     const uint32_t pd[4] = {pdv.x, pdv.y, pdv.z, pdv.w};
-    uint32_t c[16], l[16];
 #define EC_B8(j) (((j) & 3) ? (wd[(j) >> 2] >> (8 * ((j) & 3) - 3)) & 0x7F8u : (wd[(j) >> 2] << 3) & 0x7F8u)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(j));
-      c[j] = cj.x;
-      l[j] = cj.y + ((pd[j >> 2] >> (8 * (j & 3))) & 0xFFu);  // (+ the pad at a string's last byte)
-    }
-    // pairs {pc, pl}: MSB-aligned, < 32 bits; quads {qh, ql}: < 64 bits
-    uint32_t pc[8], pl[8], plx = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      pl[k] = l[2 * k] + l[2 * k + 1];
-      pc[k] = c[2 * k] | (c[2 * k + 1] >> l[2 * k]);
-      plx = max(plx, pl[k]);
-    }
-    uint32_t qh[4], qo[4], ql[4];
+    // per input dword: four codes (+ the pad at a string's last byte) ->
+    // two pairs {pc, pl} (MSB-aligned, < 32 bits) -> one quad {qh:qo, ql}
+    uint32_t qh[4], qo[4], ql[4], plx = 0;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      ql[m] = pl[2 * m] + pl[2 * m + 1];
-      qh[m] = pc[2 * m] | (pc[2 * m + 1] >> pl[2 * m]);
-      qo[m] = __builtin_amdgcn_alignbit(pc[2 * m + 1], 0u, pl[2 * m]);
+      uint32_t c[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(4 * m + u));
+        c[u] = cj.x;
+        l[u] = cj.y + ((pd[m] >> (8 * u)) & 0xFFu);
+      }
+      const uint32_t pl0 = l[0] + l[1], pl1 = l[2] + l[3];
+      const uint32_t pc0 = c[0] | (c[1] >> l[0]), pc1 = c[2] | (c[3] >> l[2]);
+      plx = max(plx, max(pl0, pl1));
+      ql[m] = pl0 + pl1;
+      qh[m] = pc0 | (pc1 >> pl0);
+      qo[m] = __builtin_amdgcn_alignbit(pc1, 0u, pl0);
+      if (EC_SB && (m & 1)) __builtin_amdgcn_sched_barrier(0);  // (bounds the lookups in flight)
     }
     const uint32_t S = act ? ql[0] + ql[1] + ql[2] + ql[3] : 0u;
     const bool longp = __ballot(act && plx > 31u) != 0;  // a pair of 32 bits or more: bytewise
     // ---- the first chunk's bytes before A go before the wave's first bit
+    // (no pads there)
     uint32_t RA = 0;
     if (first) {
       const uint32_t k = A & 15u;
       uint32_t ra = 0;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) ra += (uint32_t)j < k ? l[j] : 0u;
+      for (int j = 0; j < 15; ++j)
+        if ((uint32_t)j < k) ra += ((const uint2 *)((const char *)codeT + EC_B8(j)))->y;
       RA = __builtin_amdgcn_readfirstlane(ra);
     }
     const uint32_t Sinc = wave_incl_scan(S);
@@ -961,14 +964,19 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
           ec_or3(img, b, qh[m], qo[m]);
           b += ql[m];
         }
-      } else {
+      } else {  // a code of <= 37 bits, MSB-aligned in 64; one dword at a time
         uint32_t b = ib0;
+#pragma unroll 1
+        for (uint32_t m = 0; m < 4u; ++m) {
+          const uint32_t w = m == 0 ? wd[0] : m == 1 ? wd[1] : m == 2 ? wd[2] : wd[3];
+          const uint32_t pw = m == 0 ? pd[0] : m == 1 ? pd[1] : m == 2 ? pd[2] : pd[3];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {  // a code of <= 37 bits, MSB-aligned in 64
-          const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(j));
-          const uint32_t lj = cj.y + ((pd[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-          ec_or3(img, b, cj.x, 0u);
-          b += lj;
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t b8 = u ? (w >> (8 * u - 3)) & 0x7F8u : (w << 3) & 0x7F8u;
+            const uint2 cj = *(const uint2 *)((const char *)codeT + b8);
+            ec_or3(img, b, cj.x, 0u);
+            b += cj.y + ((pw >> (8 * u)) & 0xFFu);
+          }
         }
       }
     }
