@@ -1741,6 +1741,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_BB
 #define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
 #endif
+#ifndef DD_WSYNC
+#define DD_WSYNC 1  // warm-ups end with boundary-only single steps (no careful steps)
+#endif
 #ifndef DD_W16
 #define DD_W16 0  // a step's two symbol bytes as one unaligned ds_write_b16
 #endif
@@ -1843,7 +1846,7 @@ struct DDRun {
     k += t_ ? 1u : 0u;                                                   \
     nxt = ib[dd_phys(k)];                                                \
   } while (0)
-template <class Sink>
+template <class Sink, bool SYNC = false>
 __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
                                         uint32_t *dctr DD_SARGS) {
@@ -1900,6 +1903,34 @@ __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, u
   }
 #undef DD_SLOW
   WSTAMP(10);
+  if (SYNC) {
+    // a warm-up only needs the first codeword boundary >= bstop: single
+    // steps that take a 2-symbol entry's second symbol only while the first
+    // ends before bstop.  EOS, or a code that would pass the string end,
+    // leaves the entry unknown (failed; the verify re-decodes the item).
+    bool done = failed || (int32_t)bp >= (int32_t)bstop;
+    while (__ballot(!done)) {
+      if (!done) {
+        DCTR(2);
+        const uint32_t w = (uint32_t)(bb >> 32);
+        uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
+        if (e == 0u) e = slow_entry(T, w, 30u);
+        const uint32_t L1 = E_L1(e), adv = bp + L1 >= bstop ? L1 : E_USED(e);
+        if (e == 0xFFFFFFFFu || bp + adv > bend) {
+          failed = true;
+          done = true;
+        } else {
+          bb <<= adv;
+          bp += adv;
+          nb -= adv;
+          DD_REFILL();
+          done = bp >= bstop;
+        }
+      }
+    }
+    r.failed = failed;
+    return r;
+  }
   // careful steps: each one predicated on the stop rules instead of branching
   // -- a step takes its first symbol only if the code ends inside the string
   // (L1 <= rem), its second only if that one does too and the first ended
@@ -2419,7 +2450,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       if (spec) {
         uint32_t bp = 8u * (s - DD_OV - IBX);
         DiscardSink dk;
-        const DDRun rw = dd_run(S.T, ibe, bp, bs, bend, dk, dctr DD_SPASS);
+        const DDRun rw = dd_run<DiscardSink, DD_WSYNC != 0>(S.T, ibe, bp, bs, bend, dk, dctr DD_SPASS);
         entry = bp;
         dead = rw.failed;
       }
