@@ -338,7 +338,7 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     ms_per_step = elapsed / args.steps * 1e3
     value = B_total * args.steps / elapsed / 1e9
 
-    # roofline of the dominant kernel: k_decode (one launch per step; the
+    # roofline of the dominant kernel: k_decode_items (one launch per step; the
     # encode is two launches, k_enc_count + k_encode, reported beside it).
     # traffic: PMC-measured HBM bytes per launch of the same kernel on the
     # same config (profiles/traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per
@@ -346,9 +346,9 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     dec_alg = raw_bytes + enc_total + 12 * n  # reads E + offsets, writes R + status
     enc_alg = raw_bytes + enc_total + 12 * n
     achieved = dec_alg / t_dec / 1e9
-    roof = {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 2),
+    roof = {"bound": "hbm", "kernel": "k_decode_items", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic_for(cfg, n, "k_decode"), "alg_bytes_per_launch": dec_alg,
+            "traffic": traffic_for(cfg, n, "k_decode_items"), "alg_bytes_per_launch": dec_alg,
             "launch_ms": round(t_dec * 1e3, 4), "enc_ms": round(t_enc * 1e3, 4),
             "enc_achieved": round(enc_alg / t_enc / 1e9, 2)}
 
@@ -500,10 +500,10 @@ def run_decode_only(args, torch, dist, nghttp2_amd, W, dev, world, rank, allredu
                       "failing_strings": int((st < 0).sum()),
                       "parallelism": "shard%d (independent batches, no collective)" % world,
                       "streams": len(pipes)},
-           "roofline": {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 2),
+           "roofline": {"bound": "hbm", "kernel": "k_decode_items", "achieved": round(achieved, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                        "traffic": traffic_for(5, n, "k_decode"),
+                        "traffic": traffic_for(5, n, "k_decode_items"),
                         "alg_bytes_per_launch": B_rank, "launch_ms": round(t_dec * 1e3, 4)}}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         info = cpu_info()

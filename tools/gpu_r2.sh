@@ -31,7 +31,7 @@ for s in ${STEPS:-pytest smoke bench bench5 prof}; do
               # are the isolated durations the roofline uses
               run prof$c 300 rocprofv3 --kernel-trace --stats -d $O/prof$c -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --streams 1 --config $c
             done ;;
-    pmc)    for c in ${PMC_CFGS:-3 2}; do
+    pmc)    for c in ${PMC_CFGS:-3 2 5}; do
               rm -rf $O/pmc_c$c
               run pmc_c${c}_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_c$c/p1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 5 --warmup 2 --streams 1 --config $c
               run pmc_c${c}_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_c$c/p2 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 5 --warmup 2 --streams 1 --config $c

@@ -9,7 +9,7 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-KERNELS = ("k_decode", "k_encode", "k_enc_count", "k_scan_tiles")
+KERNELS = ("k_decode_items", "k_encode", "k_enc_count")
 
 
 def per_launch(d, counter):
@@ -32,7 +32,7 @@ def per_launch(d, counter):
 def main():
     out_path = os.path.join(ROOT, "profiles", "traffic.json")
     res = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    for cfg, strings in ((2, 1 << 20), (3, 1 << 20)):
+    for cfg, strings in ((2, 1 << 20), (3, 1 << 20), (5, 1 << 20)):
         d = os.path.join(ROOT, "gpurun_out", "pmc_c%d" % cfg)
         if not os.path.isdir(d):
             continue
