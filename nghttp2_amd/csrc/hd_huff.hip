@@ -7,21 +7,29 @@
 // MFMA): HBM-bound streaming with the code tables staged in LDS.
 //
 // Kernels
-//   k_enc_count   one string per lane: E = ceil(sum of code lengths / 8),
-//                 plus the per-256-string tile sum for the offset scan
-//   k_scan_tiles  exclusive scan of the tile sums (one workgroup)
-//   k_encode      tile scan -> encoded offsets, then MSB-first bit packing
-//                 into aligned 32-bit words with EOS-prefix (all ones)
-//                 padding (lib/nghttp2_hd_huffman.c:57-101)
-//   k_decode      persistent workgroups, one string per lane: canonical
-//                 decode with a 12-bit / 2-symbol lookup table in LDS and an
-//                 unrolled compare ladder for codes > 12 bits; the final
-//                 {fstate, flags} of the reference's nibble FSM
-//                 (lib/nghttp2_hd_huffman.c:122-136) is rebuilt exactly from
-//                 the undecoded tail bits (DESIGN.md "decode state")
-//   k_decode_fsm  the reference's nibble FSM itself (257x16 table in LDS),
-//                 kept as the exact cross-check path and for chunked calls
-//   k_slot_len / k_scan_apply   tight decode slots (floor(8E/5)+1 each)
+//   k_enc_count     aligned 16-byte chunks of a wave's 64 strings, one per
+//                   lane: code bits per string from in-chunk prefixes (LDS)
+//                   and a wave scan; per-256-string tile sums
+//   k_encode        tile offsets from the tile sums, then bit packing: each
+//                   string's EOS-prefix padding (lib/nghttp2_hd_huffman.c:
+//                   95-101) counted as length of its last byte, codes combined
+//                   into pairs and quads in registers and OR'ed into an LDS
+//                   image that leaves as whole big-endian dwords
+//   k_decode_items  decode_batch_auto: persistent waves, tasks of 64 strings,
+//                   rounds of 64 items (a string, or a 40/64-byte piece of a
+//                   long one, warmed up and verified); a 14-bit two-symbol
+//                   lookup in LDS and a register bit buffer; symbols through
+//                   a per-lane LDS region, stored back to back per task; the
+//                   final {fstate, flags} of the reference's nibble FSM
+//                   (lib/nghttp2_hd_huffman.c:122-136) rebuilt exactly from
+//                   the undecoded tail bits (DESIGN.md "decode state")
+//   k_decode        caller slots (decode_batch), and the round-1 engine-slot
+//                   kernel kept for A/B
+//   k_decode_fsm    the reference's nibble FSM itself (257x16 table in LDS),
+//                   kept as the exact cross-check path and for chunked calls
+//   k_slot_len / k_scan_tiles / k_scan_apply   tight decode slots
+//                   (floor(8E/5)+1 each)
+//   k_frame_len / k_frame_copy   HPACK string literals (emit_string)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
