@@ -1749,6 +1749,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_BB
 #define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
 #endif
+#ifndef DD_CSTORE
+#define DD_CSTORE 1  // item decoder, 64-byte items (2: all): a round's output compacted in
+                     // LDS, then coalesced stores (measured slower with 40-byte items)
+#endif
 #ifndef DD_WSYNC
 #define DD_WSYNC 1  // warm-ups end with boundary-only single steps (no careful steps)
 #endif
@@ -1787,7 +1791,7 @@ template <uint32_t IP, int IW>
 struct DIShared {  // k_decode_items
   DecTables T;  // first: the lookup at LDS offset 0
   alignas(16) uint32_t ib[IW][di_ibw(IP)];
-  uint32_t ob[IW][WAVE * di_rb(IP) / 4 + 1];
+  alignas(16) uint32_t ob[IW][(WAVE * di_rb(IP) / 4 + 1 + 3) & ~3u];
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
 };
@@ -2372,6 +2376,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
     const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
+    uint32_t ocarry = 0;  // the partial last output word of the round before
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
     for (uint32_t r0 = 0; r0 < M; r0 += WAVE) {
@@ -2517,7 +2522,84 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
       WSTAMP(5);
-      if (!DD_ABL_NOSTORE) {
+      if (!DD_ABL_NOSTORE && DD_CSTORE && (IP >= 64u || DD_CSTORE == 2)) {
+        // The round's bytes are the task's output [R0g, R1g): each lane moves
+        // its region into the round's global dwords [W0, W1), laid out back
+        // to back over the regions (realigned by alignbyte; the words shared
+        // by two lanes OR'ed), then the wave stores them 16 bytes per lane.
+        // The partial last word is carried into the next round (the task's
+        // last one is written whole: the next task starts 4-aligned).
+        const uint32_t Tot = __builtin_amdgcn_readlane(Tinc, 63);
+        const uint64_t R0g = tbase + run, R1g = R0g + Tot, W0 = R0g >> 2;
+        const uint64_t g0 = tbase + O_l;
+        const uint32_t h = (uint32_t)((4u - (g0 & 3u)) & 3u);  // bytes before alignment
+        const uint32_t nfull = V >= h ? (V - h) >> 2 : 0u;      // whole dwords
+        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(nfull), 63);
+        const uint32_t d0 = my_ob32[0];
+        const uint32_t vt = __builtin_amdgcn_alignbyte(my_ob32[nfull + 1u], my_ob32[nfull], h);
+        uint32_t d[di_rb(IP) / 4 + 1];
+#pragma unroll
+        for (uint32_t m0 = 0; m0 <= di_rb(IP) / 4; m0 += 4) {
+          if (m0 > mx) break;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            if (m0 + j <= di_rb(IP) / 4) d[m0 + j] = my_ob32[m0 + j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lds_u32 *D = (lds_u32 *)S.ob[wv];
+        const uint32_t nwr = (uint32_t)(((R1g + 3u) >> 2) - W0);  // the round's words
+        for (uint32_t i = lane; i < nwr; i += WAVE) D[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0 && ocarry) atomicOr((uint32_t *)&D[0], ocarry);
+        if (V) {
+          const uint32_t wb = (uint32_t)((g0 >> 2) - W0);
+          if (h) {  // my first bytes share a word with the lanes before
+            const uint32_t nh = min(h, V);
+            const uint32_t mk = (nh == 4u ? 0xFFFFFFFFu : (1u << (8u * nh)) - 1u) << (8u * (4u - h));
+            atomicOr((uint32_t *)&D[wb], (d0 << (8u * (4u - h))) & mk);
+          }
+          const uint32_t wf = wb + (h ? 1u : 0u);
+#pragma unroll
+          for (uint32_t m0 = 0; m0 < di_rb(IP) / 4; m0 += 4) {
+            if (m0 >= mx) break;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+              const uint32_t m = m0 + j;
+              if (m < di_rb(IP) / 4 && m < nfull) D[wf + m] = __builtin_amdgcn_alignbyte(d[m + 1u], d[m], h);
+            }
+          }
+          const uint32_t xt = h + 4u * nfull;
+          if (V > xt) atomicOr((uint32_t *)&D[wf + nfull], vt & ((1u << (8u * (V - xt))) - 1u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool lastr = r0 + WAVE >= M;
+        const uint32_t nst = lastr ? nwr : (uint32_t)((R1g >> 2) - W0);
+        for (uint32_t i4 = 4u * lane; i4 < nst; i4 += 4u * WAVE) {
+          const uint64_t gq = 4ull * (W0 + i4);
+          if (i4 + 4u <= nst && gq + 16u <= dst_cap) {
+            const u32x4 v = *(const lds_u32x4 *)(D + i4);
+            *reinterpret_cast<uint4 *>(dst + gq) = make_uint4(v.x, v.y, v.z, v.w);
+          } else {
+            for (uint32_t u = 0; u < 4u && i4 + u < nst; ++u) {
+              const uint32_t v = D[i4 + u];
+              const uint64_t q = gq + 4u * u;
+              if (q + 4u <= dst_cap) {
+                *reinterpret_cast<uint32_t *>(dst + q) = v;
+              } else {
+                for (uint32_t y = 0; y < 4u; ++y)
+                  if (q + y < dst_cap) dst[q + y] = (uint8_t)(v >> (8u * y));
+              }
+            }
+          }
+        }
+        ocarry = (!lastr && nst < nwr) ? __builtin_amdgcn_readfirstlane(D[nst]) : 0u;
+      } else if (!DD_ABL_NOSTORE) {
         // dwords realigned to the output (alignbyte) for as many dwords as
         // the wave's longest region, four per step; the bytes before the
         // first aligned dword and after the last one stored singly
