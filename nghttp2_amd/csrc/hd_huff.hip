@@ -2386,17 +2386,22 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // this lane's item: its string i = the last one with X_i <= q; every
       // string with an item in the round marks its first one (or item 0 of
       // the round), then a max-scan over the lanes
-      smap[lane] = 0u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (sl && P_l > r0 && X_l < r0 + WAVE) smap[X_l > r0 ? X_l - r0 : 0u] = lane + 1u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint32_t i = min(wave_incl_max(smap[lane]), nstr) - 1u;
-      const uint32_t k = q - __shfl(X_l, i, 64);
-      const uint32_t a = __shfl(a_l, i, 64), b = __shfl(b_l, i, 64);
+      // (a task of single-item strings: item = string, no map)
+      uint32_t i = lane, k = 0, a = a_l, b = b_l;
+      if (M != nstr) {
+        smap[lane] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (sl && P_l > r0 && X_l < r0 + WAVE) smap[X_l > r0 ? X_l - r0 : 0u] = lane + 1u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        i = min(wave_incl_max(smap[lane]), nstr) - 1u;
+        k = q - __shfl(X_l, i, 64);
+        a = __shfl(a_l, i, 64);
+        b = __shfl(b_l, i, 64);
+      }
       const uint32_t s = a + IP * k, e = min(b, s + IP);
       const bool last = e == b;
       const bool spec = valid && k > 0;
