@@ -1045,20 +1045,28 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
 // decode: canonical multi-symbol decoder
 // ---------------------------------------------------------------------------
 #define HD_COUNT_ROW(LEN, LIM, FIRST, BASE) +1
-enum { NLONG = 0 HD_HUFF_LONG_CODES(HD_COUNT_ROW) };  // code lengths > HD_HUFF_LUT_BITS
+enum {  // code lengths longer than the lookup (14-bit primary set, 13-bit set)
+  NLONG = 0 HD_HUFF_LONG_CODES(HD_COUNT_ROW),
+  NLONG13 = 0 HD_HUFF_LONG_CODES13(HD_COUNT_ROW)
+};
 #undef HD_COUNT_ROW
 
 #define NLONG_PAD 16  // search width (padding rows repeat the last row)
-static_assert(NLONG <= NLONG_PAD, "long-code search too narrow");
+static_assert(NLONG <= NLONG_PAD && NLONG13 <= NLONG_PAD, "long-code search too narrow");
 // Lookup entry (tools/gen_tables.py): sym1 | sym2 << 8 | 8 cnt << 16 | L1 << 21 | used << 27
 // (sym2 = 0 when cnt = 1: the low half is the entry's output bytes as they stand)
 #define E_CNT8(e) (((e) >> 16) & 0x18u)
 #define E_CNT(e) (((e) >> 19) & 3u)
 #define E_L1(e) (((e) >> 21) & 31u)
 #define E_USED(e) ((e) >> 27)
-struct DecTables {
-  uint32_t lut[1 << HD_HUFF_LUT_BITS];
-  uint32_t lut2[64];               // 13..16-bit codes (second level)
+// The decoder's LDS tables for an LB-bit first-level lookup (14: 64 KB, the
+// most two-symbol entries; 13: 32 KB, which leaves room for more waves).
+template <int LB>
+struct DecT {
+  static constexpr int BITS = LB;
+  static constexpr uint32_t NL = LB == 13 ? (uint32_t)NLONG13 : (uint32_t)NLONG;
+  uint32_t lut[1 << LB];
+  uint32_t lut2[64];               // codes of LB+1..16 bits (second level)
   uint32_t long_lim[NLONG_PAD];    // exclusive left-justified limit (last: ~0)
   uint32_t long_delta[NLONG_PAD];  // canonical base - first code (mod 2^32)
   uint32_t long_len[NLONG_PAD];
@@ -1067,11 +1075,17 @@ struct DecTables {
   uint16_t depth_base[30];
   uint8_t depth_ids[256];
 };
+static_assert(HD_HUFF_LUT_BITS == 14, "primary lookup");
+typedef DecT<HD_HUFF_LUT_BITS> DecTables;
 
-__device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads) {
+template <int LB>
+__device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads) {
+  static_assert(LB == 13 || LB == 14, "lookup widths generated");
   const uint32_t t = threadIdx.x;
-  for (uint32_t i = t; i < (1u << HD_HUFF_LUT_BITS); i += nthreads) T.lut[i] = dev::hd_huff_lut[i];
-  if (t < 64) T.lut2[t] = dev::hd_huff_lut2[t];
+  const uint32_t *lut = LB == 13 ? dev::hd_huff_lut13 : dev::hd_huff_lut;
+  const uint32_t *lut2 = LB == 13 ? dev::hd_huff_lut2_13 : dev::hd_huff_lut2;
+  for (uint32_t i = t; i < (1u << LB); i += nthreads) T.lut[i] = lut[i];
+  if (t < 64) T.lut2[t] = lut2[t];
   for (uint32_t i = t; i < 257; i += nthreads) T.canon[i] = dev::hd_huff_canon_sym[i];
   if (t < 30) {
     T.depth_lo[t] = dev::hd_huff_depth_lo[t];
@@ -1085,12 +1099,16 @@ __device__ __forceinline__ void stage_dec_tables(DecTables &T, uint32_t nthreads
     T.long_delta[i] = (uint32_t)(BASE) - (uint32_t)(FIRST);                  \
     T.long_len[i] = (LEN);                                                   \
     ++i;
-    HD_HUFF_LONG_CODES(HD_LONG_ROW)
+    if (LB == 13) {
+      HD_HUFF_LONG_CODES13(HD_LONG_ROW)
+    } else {
+      HD_HUFF_LONG_CODES(HD_LONG_ROW)
+    }
 #undef HD_LONG_ROW
     for (; i < NLONG_PAD; ++i) {
       T.long_lim[i] = 0xFFFFFFFFu;
-      T.long_delta[i] = T.long_delta[NLONG - 1];
-      T.long_len[i] = T.long_len[NLONG - 1];
+      T.long_delta[i] = T.long_delta[DecT<LB>::NL - 1];
+      T.long_len[i] = T.long_len[DecT<LB>::NL - 1];
     }
   }
   __syncthreads();
@@ -1318,20 +1336,22 @@ struct CheckedDwordSink {
 // the left-justified limits (one row per code length, padded to 16 rows),
 // then the symbol.  Returns a lookup-style entry
 // (cnt 1, used = L), or ~0u when EOS (symbol 256) completes within `rem`.
-__device__ __forceinline__ uint32_t long_entry(const DecTables &T, uint32_t win, uint32_t rem) {
+template <class TT>
+__device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32_t rem) {
   uint32_t i = 0;
 #pragma unroll
   for (uint32_t step = NLONG_PAD / 2; step; step >>= 1)
     i += (T.long_lim[i + step - 1] <= win) ? step : 0u;
-  i = min(i, (uint32_t)NLONG - 1u);  // win == ~0: the 30-bit row
+  i = min(i, TT::NL - 1u);  // win == ~0: the 30-bit row
   const uint32_t L = T.long_len[i];
   const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
   if (L <= rem && sym == 256) return 0xFFFFFFFFu;
   return (L <= rem ? sym : 0u) | (8u << 16) | (L << 21) | (L << 27);
 }
 
-// First-level miss: the 13..16-bit second level, else the search.
-__device__ __forceinline__ uint32_t slow_entry(const DecTables &T, uint32_t win, uint32_t rem) {
+// First-level miss: the second level (codes of up to 16 bits), else the search.
+template <class TT>
+__device__ __forceinline__ uint32_t slow_entry(const TT &T, uint32_t win, uint32_t rem) {
   const uint32_t e = T.lut2[(win >> 16) & 63u];
   return e ? e : long_entry(T, win, rem);
 }
@@ -1749,6 +1769,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_BB
 #define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
 #endif
+#ifndef DD_XINST
+#define DD_XINST 0  // A/B builds: more item-decoder instances (decode_batch_items piece 65/41/57/37)
+#endif
 #ifndef DD_CSTORE
 #define DD_CSTORE 1  // item decoder, 64-byte items (2: all): a round's output compacted in
                      // LDS, then coalesced stores (measured slower with 40-byte items)
@@ -1787,9 +1810,9 @@ __host__ __device__ constexpr uint32_t di_ibw(uint32_t ip) {
 __host__ __device__ constexpr uint32_t di_pf(uint32_t ip) {
   return (WAVE * ip + DD_OV + 8u + 32u + 16u * WAVE - 1u) / (16u * WAVE);
 }
-template <uint32_t IP, int IW>
+template <uint32_t IP, int IW, int LB>
 struct DIShared {  // k_decode_items
-  DecTables T;  // first: the lookup at LDS offset 0
+  DecT<LB> T;  // first: the lookup at LDS offset 0
   alignas(16) uint32_t ib[IW][di_ibw(IP)];
   alignas(16) uint32_t ob[IW][(WAVE * di_rb(IP) / 4 + 1 + 3) & ~3u];
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
@@ -1858,8 +1881,8 @@ struct DDRun {
     k += t_ ? 1u : 0u;                                                   \
     nxt = ib[dd_phys(k)];                                                \
   } while (0)
-template <class Sink, bool SYNC = false>
-__device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, uint32_t &bp,
+template <class Sink, bool SYNC = false, class TT>
+__device__ __forceinline__ DDRun dd_run(const TT &T, const lds_u32 *ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
                                         uint32_t *dctr DD_SARGS) {
   (void)dctr;
@@ -1900,11 +1923,11 @@ __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, u
   } while (0)
   while ((int32_t)bp <= G2) {
     DCTR(0);
-    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - HD_HUFF_LUT_BITS)];
+    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
     sink.put_nf(e1 & 0xFFFFu, E_CNT8(e1));
     const uint32_t U1 = E_USED(e1);
     bb <<= U1;
-    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - HD_HUFF_LUT_BITS)];
+    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
     sink.put_nf(e2 & 0xFFFFu, E_CNT8(e2));
     const uint32_t U2 = E_USED(e2);
     bb <<= U2;
@@ -1925,7 +1948,7 @@ __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, u
       if (!done) {
         DCTR(2);
         const uint32_t w = (uint32_t)(bb >> 32);
-        uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
+        uint32_t e = T.lut[w >> (32 - TT::BITS)];
         if (e == 0u) e = slow_entry(T, w, 30u);
         const uint32_t L1 = E_L1(e), adv = bp + L1 >= bstop ? L1 : E_USED(e);
         if (e == 0xFFFFFFFFu || bp + adv > bend) {
@@ -1954,7 +1977,7 @@ __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, u
       const uint32_t w = (uint32_t)(bb >> 32);
       const uint32_t rem = bend - bp;
       const bool stop = bp >= bstop || rem == 0u;
-      uint32_t e = T.lut[w >> (32 - HD_HUFF_LUT_BITS)];
+      uint32_t e = T.lut[w >> (32 - TT::BITS)];
       if (e == 0u && !stop) e = slow_entry(T, w, rem);
       if (e == 0xFFFFFFFFu) {
         failed = true;  // EOS: the sticky failure state
@@ -1989,7 +2012,8 @@ __device__ __forceinline__ DDRun dd_run(const DecTables &T, const lds_u32 *ib, u
 // Status and final decode context of a string (lib/nghttp2_hd_huffman.c:
 // 135-142) from its tail: as finish_string, with the FSM state (three table
 // reads) only when the caller asked for it.
-__device__ __forceinline__ void dd_finish(const DecTables &T, bool failed, uint32_t t,
+template <class TT>
+__device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
                                           uint32_t win, uint32_t nsym, bool ovf, uint32_t j,
                                           int32_t *status, uint16_t *fstate_out,
                                           uint8_t *flags_out) {
@@ -2316,7 +2340,7 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
-template <uint32_t IP, int IW>
+template <uint32_t IP, int IW, int LB>
 __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
                                                         const uint32_t *__restrict__ off,
                                                         uint32_t n, uint8_t *__restrict__ dst,
@@ -2325,7 +2349,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
                                                         int32_t *__restrict__ status,
                                                         uint16_t *__restrict__ fstate_out,
                                                         uint8_t *__restrict__ flags_out) {
-  __shared__ DIShared<IP, IW> S;
+  __shared__ DIShared<IP, IW, LB> S;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   lds_u32 *ibw = (lds_u32 *)S.ib[wv];
   const lds_u32 *ibe = ibw;
@@ -2862,23 +2886,28 @@ extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__diag_stamp
 }
 #endif
 
-template <uint32_t IP, int IW>
+template <uint32_t IP, int IW, int LB>
 static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
                                 uint8_t *dst, size_t dst_cap, uint32_t *dst_off,
                                 int32_t *status, uint16_t *fstate, uint8_t *flags,
                                 hipStream_t st) {
-  hipLaunchKernelGGL((k_decode_items<IP, IW>),
-                     dim3(persistent_grid<k_decode_items<IP, IW>, WAVE * IW, TASK_STR * IW>(n)),
+  hipLaunchKernelGGL((k_decode_items<IP, IW, LB>),
+                     dim3(persistent_grid<k_decode_items<IP, IW, LB>, WAVE * IW, TASK_STR * IW>(n)),
                      dim3(WAVE * IW), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off,
                      status, fstate, flags);
 }
 
 // piece = 64 / 40 / 32 picks an instance; 0 picks by the batch's mean
 // encoded string length, estimated from the pool size (dst_cap is normally
-// nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 + 4 n): the strings of
-// short headers fit whole 64-byte items (no warm-up; 8 waves per CU for the
-// larger LDS regions), longer values are cut into 40-byte pieces (12 waves).
-// Every instance writes the same layout.
+// nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 + 4 n), so that most
+// strings are one item.  Header strings of up to ~48 bytes fit whole 64-byte
+// items: no warm-up or item map, and the 14-bit lookup (most two-symbol
+// steps) at 8 waves per CU.  Shorter ones (mean <= 20 bytes) fit 32-byte
+// items, and longer values are cut into 40-byte pieces; both decode with
+// the 13-bit lookup, whose 32 KB less LDS buys 16 waves per CU (measured:
+// config 3 360 vs 385 us for 40-byte items with the 14-bit lookup at 12
+// waves; the adversarial config 5 162 us in 32-byte items vs 261 in 64-byte
+// ones).  Every instance writes the same layout.
 static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n, uint8_t *dst,
                         size_t dst_cap, uint32_t *dst_off, int32_t *status, uint16_t *fstate,
                         uint8_t *flags, void *stream, int piece) {
@@ -2890,14 +2919,23 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (piece == 0) {
     const uint64_t est =
         (uint64_t)dst_cap > 4ull * n ? ((uint64_t)dst_cap - 4ull * n) * 5u / 8u : 0u;
-    piece = est <= 48ull * n ? 64 : 40;
+    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 64 : 40;
   }
+#define DI_LAUNCH(P, W, B) \
+  launch_decode_items<P, W, B>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st)
   switch (piece) {
-    case 64: launch_decode_items<64u, 8>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
-    case 40: launch_decode_items<40u, 12>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
-    case 32: launch_decode_items<32u, 14>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st); break;
+    case 64: DI_LAUNCH(64u, 8, 14); break;
+    case 40: DI_LAUNCH(40u, 16, 13); break;
+    case 32: DI_LAUNCH(32u, 16, 13); break;
+#if DD_XINST  // A/B builds: the other lookup width at the same pieces
+    case 65: DI_LAUNCH(64u, 10, 13); break;
+    case 41: DI_LAUNCH(40u, 12, 14); break;
+    case 57: DI_LAUNCH(56u, 12, 13); break;
+    case 37: DI_LAUNCH(36u, 16, 13); break;
+#endif
     default: return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   }
+#undef DI_LAUNCH
   return hip_rv(hipGetLastError());
 }
 

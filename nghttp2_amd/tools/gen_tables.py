@@ -51,7 +51,7 @@ RFC7541_LEN = [
 
 ACCEPTED = 0x01
 SYM = 0x02
-LUT_BITS = 14
+LUT_BITS = 14  # the primary lookup (a 13-bit set is generated beside it)
 FAIL_STATE = 256
 EOS = 256
 
@@ -295,13 +295,39 @@ def write_inc(t, path):
         f.write("\n".join(lines) + "\n")
 
 
+def write_lut_set(t, bits, path):
+    """The decoder tables of a second lookup width (suffix = width), appended."""
+    lines = []
+    w = lines.append
+    w("/* canonical decoder, %d-bit lookup (same entry layout) */" % bits)
+    w("HD_TBL const unsigned int hd_huff_lut%d[%d] = {" % (bits, 1 << bits))
+    for i in range(0, 1 << bits, 8):
+        w("  " + ", ".join("0x%08Xu" % e for e in t["lut"][i:i + 8]) + ",")
+    w("};")
+    w("HD_TBL const unsigned int hd_huff_lut2_%d[64] = {" % bits)
+    for i in range(0, 64, 8):
+        w("  " + ", ".join("0x%08Xu" % e for e in t["lut2"][i:i + 8]) + ",")
+    w("};")
+    w("#define HD_HUFF_LONG_CODES%d(X) \\" % bits)
+    for L, lim, fc, b in t["longc"]:
+        w("  X(%d, 0x%XULL, 0x%Xu, %du) \\" % (L, lim, fc, b))
+    w("")
+    with open(path, "a") as f:
+        f.write("\n".join(lines) + "\n")
+
+
 def main():
+    global LUT_BITS
     here = os.path.dirname(os.path.abspath(__file__))
     out = os.path.join(here, "..", "csrc", "hd_huff_tables.inc")
     if len(sys.argv) > 1:
         out = sys.argv[1]
     t = build()
     write_inc(t, out)
+    primary = LUT_BITS
+    LUT_BITS = 13
+    write_lut_set(build(), 13, out)
+    LUT_BITS = primary
     sym, dec = packed_ref_layout(t)
     print("sym sha256", hashlib.sha256(sym).hexdigest())
     print("fsm sha256", hashlib.sha256(dec).hexdigest())

@@ -37,8 +37,15 @@ def main():
             "pieces": L0.nghttp2_amd_hd__decode_batch_pieces}
     for pc in (64, 40, 32):
         kern["items%d" % pc] = (lambda pc: lambda *a: L0.nghttp2_amd_hd__decode_batch_items(*a, pc))(pc)
+    for p in sorted(glob.glob(os.path.join(HERE, "lib_x*.so"))):  # extra instances (DD_XINST builds)
+        Lx = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+        Lx.nghttp2_amd_hd__decode_batch_items.argtypes = ARGS + [ctypes.c_int]
+        for pc in (65, 41, 57, 37):
+            kern["%s_%d" % (os.path.basename(p)[4:-3], pc)] = (
+                lambda L_, pc: lambda *a: L_.nghttp2_amd_hd__decode_batch_items(*a, pc))(Lx, pc)
     for p in sorted(glob.glob(os.path.join(HERE, "lib_*.so"))):
-        kern[os.path.basename(p)[4:-3]] = load(p).nghttp2_amd_hd_huff_decode_batch_auto
+        if not os.path.basename(p).startswith("lib_x"):
+            kern[os.path.basename(p)[4:-3]] = load(p).nghttp2_amd_hd_huff_decode_batch_auto
     out = {}
     for cfg in cfgs:
         if cfg == 5:
@@ -65,7 +72,14 @@ def main():
                          ctypes.c_void_p(d.data_ptr()), cap, ctypes.c_void_p(do.data_ptr()),
                          ctypes.c_void_p(st.data_ptr()), None, None, ctypes.c_void_p(s.cuda_stream))
             assert rv == 0, (k, rv)
-        for k in kern:
+        for k in list(kern):
+            d, do, st = bufs[k]
+            rv = kern[k](ctypes.c_void_p(enc.data_ptr()), ctypes.c_void_p(eo.data_ptr()), n,
+                         ctypes.c_void_p(d.data_ptr()), cap, ctypes.c_void_p(do.data_ptr()),
+                         ctypes.c_void_p(st.data_ptr()), None, None, ctypes.c_void_p(s.cuda_stream))
+            if rv != 0:  # (an instance this build does not have)
+                del kern[k]
+                continue
             for _ in range(3):
                 run(k)
         torch.cuda.synchronize()
