@@ -1769,6 +1769,12 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_BB
 #define DD_BB 1  // fast steps from a register bit buffer (else LDS windows)
 #endif
+#ifndef DD_BALANCE
+#define DD_BALANCE 1  // item decoder (40-byte pieces): weight-balanced task ranges per workgroup
+#endif
+#ifndef DD_TASK_W
+#define DD_TASK_W 32u  // item decoder: a string's weight in bytes when balancing tasks
+#endif
 #ifndef DD_XINST
 #define DD_XINST 0  // A/B builds: more item-decoder instances (decode_batch_items piece 65/41/57/37)
 #endif
@@ -2362,7 +2368,36 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
   uint32_t dctr[4] = {0, 0, 0, 0};
   (void)dctr;
-  const uint32_t tstride = gridDim.x * IW;
+  // this workgroup's tasks: with 40-byte pieces (long values, whose tasks
+  // differ several-fold in work) a contiguous range balanced by weight
+  // (encoded bytes + DD_TASK_W per string) over the grid, its waves striding
+  // over it (config 3: 348 vs 356 us); else the grid strides over all tasks
+  // (the search costs a short batch more than it saves)
+  constexpr bool kBal = DD_BALANCE && IP == 40u;
+  uint32_t t_lo, t_hi;
+  {
+    const uint32_t nwg = gridDim.x, g = blockIdx.x;
+    const uint64_t wtot = (uint64_t)(off[n] - off0) + (uint64_t)DD_TASK_W * n;
+    auto first_at = [&](uint64_t target) -> uint32_t {  // smallest t with weight(t) >= target
+      if (target == 0) return 0u;
+      uint32_t lo = 0, hi = ntask;  // weight(lo) < target <= weight(hi)
+      while (hi - lo > 1u) {
+        const uint32_t step = (hi - lo + WAVE - 1u) / WAVE;
+        const uint32_t c = min(lo + (lane + 1u) * step, hi);
+        const uint32_t sc = min(c * (uint32_t)TASK_STR, n);
+        const uint64_t wc = (uint64_t)(off[sc] - off0) + (uint64_t)DD_TASK_W * sc;
+        const uint64_t ge = __ballot(wc >= target);  // (lane 63 or the clamp reaches hi)
+        const uint32_t j = ge ? (uint32_t)__builtin_ctzll(ge) : WAVE - 1u;
+        const uint32_t nhi = __builtin_amdgcn_readlane(c, j);
+        lo = j ? __builtin_amdgcn_readlane(c, j - 1u) : lo;
+        hi = nhi;
+      }
+      return hi;
+    };
+    t_lo = kBal ? first_at(wtot * g / nwg) : g * IW;
+    t_hi = kBal ? (g + 1u == nwg ? ntask : first_at(wtot * (g + 1u) / nwg)) : ntask;
+  }
+  const uint32_t t_first = t_lo + wv, t_step = kBal ? (uint32_t)IW : gridDim.x * IW;
   // a task's string offsets are loaded one task ahead, and the first round
   // of the next task is staged into registers during the current task's last
   // round (pf), so neither waits at a task start
@@ -2383,8 +2418,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   };
   uint4 pf[di_pf(IP)];
   uint32_t pf_IB = 0xFFFFFFFFu;
-  load_offs(blockIdx.x * IW + wv);
-  for (uint32_t task = blockIdx.x * IW + wv; task < ntask; task += tstride) {
+  load_offs(t_first < t_hi ? t_first : ntask);
+  for (uint32_t task = t_first; task < t_hi; task += t_step) {
     WCOUNT(8);
     const uint32_t t0 = task * TASK_STR;
     const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
@@ -2392,7 +2427,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     const uint32_t a_l = na_l, b_l = nb_l;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
-    load_offs(task + tstride);
+    load_offs(task + t_step < t_hi ? task + t_step : ntask);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
     // items: m_l of string l, X_l the first
@@ -2463,10 +2498,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         if (r0 + WAVE < M) {
           round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), A, Z, IBn, ncn);
           pf_IB = IBn;
-        } else if (task + tstride < ntask) {
+        } else if (task + t_step < t_hi) {
           const uint32_t An = __builtin_amdgcn_readfirstlane(na_l);
           const uint32_t Zn = __builtin_amdgcn_readlane(
-              nb_l, min(n - (task + tstride) * TASK_STR, (uint32_t)TASK_STR) - 1u);
+              nb_l, min(n - (task + t_step) * TASK_STR, (uint32_t)TASK_STR) - 1u);
           round_range(An, An, Zn, IBn, ncn);
           pf_IB = IBn;
         }
