@@ -2965,8 +2965,10 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
 #if DD_XINST  // A/B builds: the other lookup width at the same pieces
     case 65: DI_LAUNCH(64u, 10, 13); break;
     case 41: DI_LAUNCH(40u, 12, 14); break;
-    case 57: DI_LAUNCH(56u, 12, 13); break;
-    case 37: DI_LAUNCH(36u, 16, 13); break;
+    case 44: DI_LAUNCH(44u, 15, 13); break;
+    case 33: DI_LAUNCH(32u, 14, 14); break;
+    case 36: DI_LAUNCH(36u, 13, 14); break;
+    case 30: DI_LAUNCH(30u, 15, 14); break;
 #endif
     default: return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   }
