@@ -90,10 +90,11 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, u
  * nghttp2_amd_hd_huff_decode_slots need for `n` strings. */
 NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n);
 
-/* Workspace that lets nghttp2_amd_hd_huff_encode_batch keep per-piece bit
- * counts from its count pass for its pack pass (faster; same output) for
+/* A workspace size for nghttp2_amd_hd_huff_encode_batch that is also valid
+ * for earlier versions of the library, which kept per-piece bit counts for
  * `raw_bytes` raw bytes in `n` strings.  Any size >=
- * nghttp2_amd_hd_huff_workspace_size(n) is valid. */
+ * nghttp2_amd_hd_huff_workspace_size(n) is valid; the current kernels use
+ * only that much. */
 NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw_bytes, uint32_t n);
 
 /* ------------------------------------------------------------------ */
@@ -109,8 +110,7 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw
  *   dst               : encoded pool (device), >= dst_cap bytes
  *   dst_off[n+1]      : OUT: encoded string i = dst[dst_off[i]..dst_off[i+1]);
  *                       dst_off[i+1]-dst_off[i] == nghttp2_hd_huff_encode_count
- *   workspace         : device scratch, >= nghttp2_amd_hd_huff_workspace_size(n);
- *                       nghttp2_amd_hd_huff_encode_workspace_size(raw, n) is faster
+ *   workspace         : device scratch, >= nghttp2_amd_hd_huff_workspace_size(n)
  *
  * Output bytes equal lib/nghttp2_hd_huffman.c's, including the EOS-prefix
  * (all ones) padding of the last byte.  Size dst_cap by
@@ -198,17 +198,22 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, cons
                                      void *stream);
 
 /*
- * Same as nghttp2_amd_hd_huff_decode_batch, with the engine assigning the
- * output slots in the same launch: with x_i = src_off[i] - src_off[0],
- * dst_off[i] = 4 * (ceil(floor(8 x_i / 5) / 4) + i) (OUT, n+1 entries).
- * Slots are 4-byte aligned and each holds at least floor(8*E_i/5)+1 bytes
- * -- the reference's allocation -- so no string can overflow; bytes of a
- * slot past its decoded length are unspecified.  dst (16-byte aligned) must
- * hold nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes; strings whose slot
- * would end past dst_cap get -502, write nothing, and their dst_off entries
- * saturate at dst_cap.  Slots are uint32 offsets: dst_cap > 0xFFFFFFFF
- * returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT (split a batch whose
- * decode_bound passes 4 GiB).
+ * Same as nghttp2_amd_hd_huff_decode_batch, with the engine placing the
+ * output in the same launch, densely: the strings of each task of 64
+ * consecutive strings (t0 = 64 k) are back to back from the task's base
+ *   base(t0) = 4 * (ceil(floor(8 x_t0 / 5) / 4) + t0),  x_t0 = src_off[t0] - src_off[0],
+ * so dst_off[i] (OUT, n+1 entries) = base(t0) + the decoded bytes of the
+ * task's strings before i, and dst_off[n] = the end of the last string.
+ * Every string keeps the reference's allocation inside its task's span
+ * (base(t0 + 64) - base(t0) >= the sum of floor(8 E_i / 5) + 1), so no
+ * string can overflow; bytes between the end of a task's output and the
+ * next task's base are unspecified.  dst (16-byte aligned) must hold
+ * nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes.  String i gets -502
+ * when 4 * (ceil(floor(8 x_{i+1} / 5) / 4) + i + 1) > dst_cap (a pool
+ * smaller than the bound); no byte at or past dst_cap is written and dst_off
+ * entries saturate at dst_cap.  Offsets
+ * are uint32: dst_cap > 0xFFFFFFFF returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT
+ * (split a batch whose decode_bound passes 4 GiB).
  */
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint8_t *dst, size_t dst_cap,
