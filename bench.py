@@ -152,6 +152,18 @@ def verify_roundtrip(dec, dec_off, pool, off, chunk=1 << 18):
         got = dec[lo:hi].cpu().numpy()[idx - lo] if tot else np.zeros(0, np.uint8)
         if not np.array_equal(got, pool[off64[a]:off64[b]]):
             raise AssertionError("decode(encode(x)) != x in strings [%d, %d)" % (a, b))
+        if (a // chunk) % 16 == 15:
+            progress("checked %d of %d strings" % (b, n))
+
+
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (long runs: config 4 generates and checks 16M
+    strings); stdout keeps the one JSON line."""
+    if os.environ.get("RANK", "0") == "0":
+        print("[bench %7.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
 
 
 def main():
@@ -203,10 +215,12 @@ def main():
         return pool, off, "strong", "numpy PCG64, chunk-seeded 0x%X, shard [%d, %d) of %d" % (
             W.SEED[4], s0, s1, n_total)
 
+    progress("config %d, %d rank(s), backend %s" % (cfg, world, backend))
     if cfg == 5:
         out = run_decode_only(args, torch, dist, nghttp2_amd, W, dev, world, rank, allreduce)
     else:
         pool, off, scaling, data = gen(cfg, rank)
+        progress("generated %d strings, %d bytes" % (len(off) - 1, int(off[-1])))
         out, ctx = run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce,
                                  pool, off, cfg, scaling, data)
         if cfg == 3 and not args.no_secondary:
@@ -218,6 +232,7 @@ def main():
                 workload=CONFIG_NAMES[2], strings_per_gpu=sec["config"]["strings_per_gpu"],
                 raw_bytes_per_gpu=sec["config"]["raw_bytes_per_gpu"], roofline=sec["roofline"])
         if rank == 0 and not args.no_cpu_baseline and world == 1:
+            progress("cpu baseline")
             info = cpu_info()
             threads = args.cpu_threads or info["usable"]
             ns = min(len(off) - 1, CPU_SAMPLE)
@@ -252,8 +267,10 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     enc_cap = codec0.encode_bound(raw_bytes, n)
     probe_enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
     probe_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    progress("config %d: inputs on the device" % cfg)
     codec0.encode(src, src_off, raw_bytes=raw_bytes, dst=probe_enc, dst_off=probe_off)
     enc_total = int(probe_off[-1].item()) & 0xFFFFFFFF
+    progress("config %d: encoded %d bytes" % (cfg, enc_total))
     assert enc_total != 0xFFFFFFFF, "encoded total overflows the uint32 offsets"
     del probe_enc, probe_off
     enc_cap = min(enc_cap, enc_total + 4096)  # the kernels never write past dst_cap
@@ -294,13 +311,15 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         for p in pipes:
             p.run()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        progress("config %d: warm-up step %d" % (cfg, w))
     for p in pipes[1:]:  # every pipe decodes the batch exactly
         assert torch.equal(p.status, P0.status) and torch.equal(p.enc_off, P0.enc_off)
 
+    progress("config %d: warm-up done, checking the round trip" % cfg)
     # correctness gate on this rank's batch (fails loudly, never measured)
     st = P0.status.cpu().numpy()
     raw_len = np.diff(off.astype(np.int64))
@@ -308,6 +327,7 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     assert int(P0.enc_off[-1].item()) & 0xFFFFFFFF == enc_total
     verify_roundtrip(P0.dec, P0.dec_off.cpu().numpy().view(np.uint32), pool, off)
 
+    progress("config %d: round trip checked, timing" % cfg)
     # per-kernel timing (roofline): K plain steps with events on the stream
     for i in range(args.steps):
         P0.run(ev[i])

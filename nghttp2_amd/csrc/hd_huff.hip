@@ -1775,6 +1775,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_TASK_W
 #define DD_TASK_W 32u  // item decoder: a string's weight in bytes when balancing tasks
 #endif
+#ifndef DD_GIN
+#define DD_GIN 0  // A/B builds: item decoders read their input through the caches, not LDS
+#endif
 #ifndef DD_XINST
 #define DD_XINST 0  // A/B builds: more item-decoder instances (decode_batch_items piece 65/41/57/37)
 #endif
@@ -1860,6 +1863,19 @@ __device__ __forceinline__ uint32_t dd_win(const lds_u32 *ib, uint32_t q) {  // 
   return __builtin_amdgcn_alignbit(ib[p], ib[p + 1], ~q);
 }
 
+// Input word k (big-endian) of a decode: the wave's staged LDS copy, or the
+// pool itself through the vector caches (DD_GIN A/B builds).
+struct LdsIn {
+  const lds_u32 *ib;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return ib[dd_phys(k)]; }
+};
+struct GlobalIn {
+  const uint8_t *base;  // byte of word 0
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(base + 4u * k));
+  }
+};
+
 struct DDRun {
   bool failed, at_end;
   uint32_t t, win;  // at the string end: tail bits and the last window
@@ -1885,10 +1901,10 @@ struct DDRun {
     bb |= (uint64_t)(t_ ? nxt : 0u) << ((32u - nb) & 63u);               \
     nb += t_ ? 32u : 0u;                                                 \
     k += t_ ? 1u : 0u;                                                   \
-    nxt = ib[dd_phys(k)];                                                \
+    nxt = ib(k);                                                         \
   } while (0)
-template <class Sink, bool SYNC = false, class TT>
-__device__ __forceinline__ DDRun dd_run(const TT &T, const lds_u32 *ib, uint32_t &bp,
+template <class Sink, bool SYNC = false, class TT, class IN>
+__device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
                                         uint32_t *dctr DD_SARGS) {
   (void)dctr;
@@ -1901,11 +1917,11 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const lds_u32 *ib, uint32_t
   int32_t G2 = min((int32_t)bstop - 27, (int32_t)bend - 28);  // last start of a fast pair
   uint32_t k = bp >> 5;
   const uint32_t o = bp & 31u;
-  const uint32_t w0 = ib[dd_phys(k)], w1 = ib[dd_phys(k + 1u)];
+  const uint32_t w0 = ib(k), w1 = ib(k + 1u);
   uint64_t bb = (((uint64_t)w0 << 32) | w1) << o;
   uint32_t nb = 64u - o;
   k += 2u;
-  uint32_t nxt = ib[dd_phys(k)];
+  uint32_t nxt = ib(k);
   // a code longer than the lookup inside the pair loop (nb >= 32): decode
   // it, or leave the pair loop at EOS (failed) or at the string's tail
   // (the careful steps find it again)
@@ -2175,7 +2191,7 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
       while (__ballot(mode != DD_DONE)) {
         WCOUNT(6);
         if (mode != DD_DONE) {
-          const DDRun rr = dd_run(S.T, ibe, bp, bstop, bend, sk, dctr DD_SPASS);
+          const DDRun rr = dd_run(S.T, LdsIn{ibe}, bp, bstop, bend, sk, dctr DD_SPASS);
           if (mode == DD_WARM) {
             // the entry: the first boundary >= 8 s, or the string's tail
             sk.n = 0;  // the warm-up's symbols belong to the lane before
@@ -2246,7 +2262,7 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
             r0.at_end = false;
           } else {
             uint32_t bq = pred;
-            const DDRun rr = dd_run(S.T, ibe, bq, bstop0, bend0, s3, dctr DD_SPASS);
+            const DDRun rr = dd_run(S.T, LdsIn{ibe}, bq, bstop0, bend0, s3, dctr DD_SPASS);
             r0.entry = pred;
             r0.exit = rr.failed ? XFAIL : bq;
             r0.t = rr.t;
@@ -2470,7 +2486,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       uint32_t IB, nchunk;
       round_range(R0, A, Z, IB, nchunk);
       const uint32_t IBX = IB - 16u;
-      {
+#if DD_GIN
+      const GlobalIn inp{src + IB - 16};
+#else
+      const LdsIn inp{ibe};
+#endif
+      if (!DD_GIN) {
         const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
         if (pf_IB != IB) {  // (not prefetched)
 #pragma unroll
@@ -2527,7 +2548,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       if (spec) {
         uint32_t bp = 8u * (s - DD_OV - IBX);
         DiscardSink dk;
-        const DDRun rw = dd_run<DiscardSink, DD_WSYNC != 0>(S.T, ibe, bp, bs, bend, dk, dctr DD_SPASS);
+        const DDRun rw = dd_run<DiscardSink, DD_WSYNC != 0>(S.T, inp, bp, bs, bend, dk, dctr DD_SPASS);
         entry = bp;
         dead = rw.failed;
       }
@@ -2537,7 +2558,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       DDRun rr;
       rr.failed = rr.at_end = false;
       rr.t = rr.win = 0;
-      if (valid && !dead) rr = dd_run(S.T, ibe, bp, bstop, bend, sk, dctr DD_SPASS);
+      if (valid && !dead) rr = dd_run(S.T, inp, bp, bstop, bend, sk, dctr DD_SPASS);
       uint32_t my_exit = rr.failed ? XFAIL : bp;
       uint32_t my_entry = dead ? XUNKNOWN : entry;
       uint32_t c0 = sk.n;
@@ -2562,7 +2583,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             my_exit = XFAIL;
           } else {
             uint32_t bq = pred;
-            rr = dd_run(S.T, ibe, bq, bstop, bend, s3, dctr DD_SPASS);
+            rr = dd_run(S.T, inp, bq, bstop, bend, s3, dctr DD_SPASS);
             my_exit = rr.failed ? XFAIL : bq;
           }
           my_entry = pred;
