@@ -211,7 +211,9 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, cons
  * nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes.  String i gets -502
  * when 4 * (ceil(floor(8 x_{i+1} / 5) / 4) + i + 1) > dst_cap (a pool
  * smaller than the bound); no byte at or past dst_cap is written and dst_off
- * entries saturate at dst_cap.  Offsets
+ * entries saturate at dst_cap.  src_off must be non-decreasing: a task
+ * holding a descending pair reports NGHTTP2_AMD_ERR_INVALID_ARGUMENT for its
+ * strings and writes nothing for them.  Offsets
  * are uint32: dst_cap > 0xFFFFFFFF returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT
  * (split a batch whose decode_bound passes 4 GiB).
  */

@@ -2446,6 +2446,16 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     load_offs(task + t_step < t_hi ? task + t_step : ntask);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
+    if (__ballot(sl && (b_l < a_l || a_l < off0))) {
+      // offsets out of order (a caller error): the task's strings report
+      // INVALID_ARGUMENT and write nothing, instead of a near-endless item walk
+      if (sl) {
+        status[t0 + lane] = NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+        dst_off[t0 + lane] = (uint32_t)min(tbase, dst_cap);
+        if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase, dst_cap);
+      }
+      continue;
+    }
     // items: m_l of string l, X_l the first
     const uint32_t m_l = sl ? max(1u, (b_l - a_l + IP - 1u) / IP) : 0u;
     const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;

@@ -138,14 +138,16 @@ class HuffmanBatchCodec:
         self._ws = None
         self._ews = None
 
-    def _workspace(self, n, raw_bytes=None):
-        if raw_bytes is None:
-            need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
-        else:
-            need = self.L.nghttp2_amd_hd_huff_encode_workspace_size(int(raw_bytes), n)
+    def _workspace(self, n, raw_bytes=None, stream=None):
+        need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
         if self._ws is None or self._ws.numel() < need:
-            # zeroed once; the engine keeps it consistent across calls (epochs)
-            self._ws = self.torch.zeros(need, dtype=self.torch.uint8, device=self.device)
+            # Uninitialised on purpose: the kernels write every workspace word
+            # they read.  (A zero fill would be a kernel on the *current*
+            # stream, unordered with a call on another stream: it once
+            # overwrote a running encode's tile sums in the two-stream bench.)
+            with self.torch.cuda.stream(stream if stream is not None
+                                        else self.torch.cuda.current_stream(self.device)):
+                self._ws = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
         return self._ws
 
     def encode_bound(self, raw_bytes, n):
@@ -162,7 +164,7 @@ class HuffmanBatchCodec:
             dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
         if dst_off is None:
             dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
-        ws = self._workspace(n, raw_bytes)
+        ws = self._workspace(n, raw_bytes, stream)
         rv = self.L.nghttp2_amd_hd_huff_encode_batch(
             _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(ws),
             ws.numel(), _stream(stream))
@@ -219,7 +221,7 @@ class HuffmanBatchCodec:
         n = src_off.numel() - 1
         if dst_off is None:
             dst_off = self.torch.empty(n + 1, dtype=self.torch.int32, device=self.device)
-        ws = self._workspace(n)
+        ws = self._workspace(n, stream=stream)
         rv = self.L.nghttp2_amd_hd_huff_decode_slots(
             _p(src_off), n, _p(dst_off), _p(ws), ws.numel(), _stream(stream))
         _check(rv, "decode_slots")

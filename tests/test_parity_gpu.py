@@ -417,3 +417,23 @@ def test_dense_decode_edges(codec, dev, piece):
         assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag
         assert np.array_equal(fl.cpu().numpy(), rfl), tag
         check_dense_layout(dst.cpu().numpy(), do.cpu().numpy().view(np.uint32), e, eo, tag)
+
+
+def test_decode_descending_offsets_refused(codec, dev):
+    """Offsets out of order (a caller error) end in INVALID_ARGUMENT for the
+    strings of the task that holds them, not in an endless item walk; the
+    other tasks decode normally."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(256, seed=5)
+    enc, eoff = O.encode_batch(pool, off)
+    bad = eoff.copy()
+    bad[70] = bad[72]  # string 70 ends before it starts (task 1: strings 64..127)
+    src = to_dev(pad16(enc, eoff[-1]), dev)
+    dst = torch.zeros(codec.decode_bound(int(eoff[-1]), 256) + 4096, dtype=torch.uint8, device=dev)
+    dst, do, st = codec.decode_auto(src, to_dev(bad, dev), dst=dst)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert (st[64:128] == -501).all()
+    rst = O.decode_batch(enc, eoff)[2]
+    assert np.array_equal(st[:64], rst[:64]) and np.array_equal(st[128:], rst[128:])
