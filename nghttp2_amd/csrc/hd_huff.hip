@@ -1853,6 +1853,20 @@ struct LdsSink {
   __device__ __forceinline__ void flush() {}
 };
 
+// The item decoder's sink: a running LDS pointer (one add per step fewer
+// than base + count).
+struct LdsPtrSink {
+  lds_u8 *p, *base;
+  __device__ __forceinline__ uint32_t count() const { return (uint32_t)(p - base); }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p += c8 >> 3;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
+  __device__ __forceinline__ void flush() {}
+};
+
 // Staged input, skewed: logical dword k lives at k + k / 8, and each block of
 // 8 is followed by a copy of the next block's first dword, so the two dwords
 // of a window are adjacent while the 64 lanes' pieces (8 dwords apart for
@@ -2549,9 +2563,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t bs = 8u * (s - IBX);
       const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
       const uint32_t bstop = last ? bend : 8u * (e - IBX);
-      LdsSink sk;
-      sk.p = my_ob;
-      sk.n = 0;
+      LdsPtrSink sk{my_ob, my_ob};
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
@@ -2571,7 +2583,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       if (valid && !dead) rr = dd_run(S.T, inp, bp, bstop, bend, sk, dctr DD_SPASS);
       uint32_t my_exit = rr.failed ? XFAIL : bp;
       uint32_t my_entry = dead ? XUNKNOWN : entry;
-      uint32_t c0 = sk.n;
+      uint32_t c0 = sk.count();
       WSTAMP(3);
       // ---- verify the later items against the previous item's exit
       for (uint32_t iter = 0; iter <= WAVE; ++iter) {
@@ -2583,9 +2595,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         DCTR(3);
         const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
         if (mism && !pred_mism) {
-          LdsSink s3;
-          s3.p = my_ob;
-          s3.n = 0;
+          LdsPtrSink s3{my_ob, my_ob};
           if (pred == XFAIL || pred == XUNKNOWN || pred == DD_NONE) {
             rr.failed = true;  // the string failed in an earlier item
             rr.at_end = false;
@@ -2597,7 +2607,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             my_exit = rr.failed ? XFAIL : bq;
           }
           my_entry = pred;
-          c0 = s3.n;
+          c0 = s3.count();
         }
       }
       WSTAMP(4);
