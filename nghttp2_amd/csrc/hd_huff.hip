@@ -1775,6 +1775,12 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_TASK_W
 #define DD_TASK_W 32u  // item decoder: a string's weight in bytes when balancing tasks
 #endif
+#ifndef DD_CLAIM
+#define DD_CLAIM 1  // item decoder: waves of a workgroup claim tasks from an LDS counter
+#endif
+#ifndef DD_CAREFUL2
+#define DD_CAREFUL2 1  // careful steps as selects (every lane steps), not exec-mask branches
+#endif
 #ifndef DD_GIN
 #define DD_GIN 0  // A/B builds: item decoders read their input through the caches, not LDS
 #endif
@@ -1826,6 +1832,7 @@ struct DIShared {  // k_decode_items
   alignas(16) uint32_t ob[IW][(WAVE * di_rb(IP) / 4 + 1 + 3) & ~3u];
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
+  uint32_t claimed;               // tasks of the workgroup's range claimed so far
 };
 
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
@@ -2007,6 +2014,38 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // (L1 <= rem), its second only if that one does too and the first ended
   // before bstop; a first code that does not fit is the string's tail
   bool done = failed;
+  if (DD_CAREFUL2) {
+    // the same steps with every lane stepping (a finished lane takes
+    // nothing): selects instead of exec-mask branches, the rare long code
+    // behind one uniform branch
+    while (__ballot(!done)) {
+      DCTR(2);
+      const uint32_t w = (uint32_t)(bb >> 32);
+      const uint32_t rem = bend - bp;
+      const bool stop = done || bp >= bstop || rem == 0u;
+      uint32_t e = T.lut[w >> (32 - TT::BITS)];
+      const bool slow = e == 0u && !stop;
+      if (__ballot(slow)) {
+        if (slow) e = slow_entry(T, w, rem);
+      }
+      const bool eos = e == 0xFFFFFFFFu && !stop;  // EOS: the sticky failure state
+      const uint32_t L1 = E_L1(e), U = E_USED(e);
+      const bool take1 = !stop && !eos && L1 <= rem;
+      const bool take2 = take1 && E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
+      const bool tail = !stop && !eos && !take1;  // a proper prefix of a code
+      r.at_end = r.at_end || tail;
+      r.t = tail ? rem : r.t;
+      r.win = tail ? w : r.win;
+      const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
+      sink.put(take2 ? (e & 0xFFFFu) : (e & 0xFFu), take2 ? 16u : (take1 ? 8u : 0u));
+      bb <<= adv;
+      bp += adv;
+      nb -= adv;
+      DD_REFILL();
+      failed = failed || eos;
+      done = done || eos || !take1 || bp >= bstop;
+    }
+  }
   while (__ballot(!done)) {
     if (!done) {
       DCTR(2);
@@ -2392,6 +2431,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
   lds_u32 *ost = (lds_u32 *)S.ostart[wv];
+  if (threadIdx.x == 0) S.claimed = 0u;
   stage_dec_tables(S.T, (WAVE * IW));  // the kernel's only workgroup barrier
   WSTAMP_INIT();
   const uint32_t off0 = off[0];
@@ -2424,10 +2464,26 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       }
       return hi;
     };
-    t_lo = kBal ? first_at(wtot * g / nwg) : g * IW;
-    t_hi = kBal ? (g + 1u == nwg ? ntask : first_at(wtot * (g + 1u) / nwg)) : ntask;
+    if (DD_CLAIM) {  // contiguous workgroup ranges (by weight or by count)
+      t_lo = kBal ? first_at(wtot * g / nwg) : (uint32_t)((uint64_t)ntask * g / nwg);
+      t_hi = g + 1u == nwg ? ntask
+                           : kBal ? first_at(wtot * (g + 1u) / nwg)
+                                  : (uint32_t)((uint64_t)ntask * (g + 1u) / nwg);
+    } else {
+      t_lo = kBal ? first_at(wtot * g / nwg) : g * IW;
+      t_hi = kBal ? (g + 1u == nwg ? ntask : first_at(wtot * (g + 1u) / nwg)) : ntask;
+    }
   }
+  // DD_CLAIM: a wave's first task is t_lo + wv, later ones are claimed from
+  // the workgroup's LDS counter one task ahead (so the waves of a CU finish
+  // within a task of each other); else a fixed stride
   const uint32_t t_first = t_lo + wv, t_step = kBal ? (uint32_t)IW : gridDim.x * IW;
+  auto claim_next = [&](uint32_t cur) -> uint32_t {
+    if (!DD_CLAIM) return cur + t_step;
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd((uint32_t *)&S.claimed, 1u);
+    return t_lo + IW + __builtin_amdgcn_readfirstlane(v);
+  };
   // a task's string offsets are loaded one task ahead, and the first round
   // of the next task is staged into registers during the current task's last
   // round (pf), so neither waits at a task start
@@ -2449,7 +2505,9 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   uint4 pf[di_pf(IP)];
   uint32_t pf_IB = 0xFFFFFFFFu;
   load_offs(t_first < t_hi ? t_first : ntask);
-  for (uint32_t task = t_first; task < t_hi; task += t_step) {
+  uint32_t next_task = t_hi;
+  for (uint32_t task = t_first; task < t_hi; task = next_task) {
+    next_task = claim_next(task);
     WCOUNT(8);
     const uint32_t t0 = task * TASK_STR;
     const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
@@ -2457,7 +2515,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     const uint32_t a_l = na_l, b_l = nb_l;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
-    load_offs(task + t_step < t_hi ? task + t_step : ntask);
+    load_offs(next_task < t_hi ? next_task : ntask);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
     if (__ballot(sl && (b_l < a_l || a_l < off0))) {
@@ -2543,10 +2601,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         if (r0 + WAVE < M) {
           round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), A, Z, IBn, ncn);
           pf_IB = IBn;
-        } else if (task + t_step < t_hi) {
+        } else if (next_task < t_hi) {
           const uint32_t An = __builtin_amdgcn_readfirstlane(na_l);
           const uint32_t Zn = __builtin_amdgcn_readlane(
-              nb_l, min(n - (task + t_step) * TASK_STR, (uint32_t)TASK_STR) - 1u);
+              nb_l, min(n - next_task * TASK_STR, (uint32_t)TASK_STR) - 1u);
           round_range(An, An, Zn, IBn, ncn);
           pf_IB = IBn;
         }
