@@ -34,6 +34,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <type_traits>
 
 #include "../../include/nghttp2_amd_hd.h"
 
@@ -1797,6 +1798,24 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_W16
 #define DD_W16 0  // a step's two symbol bytes as one unaligned ds_write_b16
 #endif
+#ifndef DD_LATE
+#define DD_LATE 0  // item decoder: the next round's input staged at the end of a round (see kLate)
+#endif
+#ifndef DD_G2OLD
+#define DD_G2OLD 0  // A/B builds: the round-2 fast-pair bound (bstop - 27, bend - 28)
+#endif
+#ifndef DD_WIN
+#define DD_WIN 0  // fast pairs from a window read per pair (else a refilled register buffer)
+#endif
+#ifndef DD_WINC
+#define DD_WINC 0  // careful steps: the window read per step (else the register buffer)
+#endif
+#ifndef DD_SLOWU
+#define DD_SLOWU 0  // fast pairs: the long-code path behind a uniform (ballot) branch
+#endif
+#ifndef DD_ACC
+#define DD_ACC 0  // item decoder: symbols gathered in a register word, one ds_write_b32 per pair
+#endif
 #define DD_NT (WAVE * DD_WAVES)
 // a lane decodes bits [8 s, 8 e + 29] at most: <= (8 P + 29) / 5 symbols,
 // plus one byte of slack (the second byte of a 1-symbol entry is written)
@@ -1819,17 +1838,25 @@ struct DDShared {
 // (<= (8 IP + 29) / 5 symbols, one byte of slack, dword aligned), the staged
 // dwords of a wave, the staged 16-byte chunks per lane
 __host__ __device__ constexpr uint32_t di_rb(uint32_t ip) { return (((8u * ip + 29u) / 5u) + 2u + 3u) & ~3u; }
-__host__ __device__ constexpr uint32_t di_ibw(uint32_t ip) {
-  return (((WAVE * ip + DD_OV + 64u) / 4u + 8u) + 3u) & ~3u;  // whole 16-byte chunks
+// A round's items span at most `span` input bytes: 64 items of IP bytes, or
+// (budgeted rounds, BI > 0) as many of the next 64 items as fit BI bytes.
+// Their output regions (di_rb of each item's bytes, laid back to back) then
+// take at most 8 BI / 5 + 64 (29 / 5 + 5) bytes.
+__host__ __device__ constexpr uint32_t di_span(uint32_t ip, uint32_t bi) { return bi ? bi : WAVE * ip; }
+__host__ __device__ constexpr uint32_t di_obb(uint32_t ip, uint32_t bi) {
+  return bi ? ((8u * bi) / 5u + 692u + 15u) & ~15u : WAVE * di_rb(ip);
 }
-__host__ __device__ constexpr uint32_t di_pf(uint32_t ip) {
-  return (WAVE * ip + DD_OV + 8u + 32u + 16u * WAVE - 1u) / (16u * WAVE);
+__host__ __device__ constexpr uint32_t di_ibw(uint32_t span) {
+  return (((span + DD_OV + 64u) / 4u + 8u) + 3u) & ~3u;  // whole 16-byte chunks
 }
-template <uint32_t IP, int IW, int LB>
+__host__ __device__ constexpr uint32_t di_pf(uint32_t span) {
+  return (span + DD_OV + 8u + 32u + 16u * WAVE - 1u) / (16u * WAVE);
+}
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
 struct DIShared {  // k_decode_items
   DecT<LB> T;  // first: the lookup at LDS offset 0
-  alignas(16) uint32_t ib[IW][di_ibw(IP)];
-  alignas(16) uint32_t ob[IW][(WAVE * di_rb(IP) / 4 + 1 + 3) & ~3u];
+  alignas(16) uint32_t ib[IW][di_ibw(di_span(IP, BI))];
+  alignas(16) uint32_t ob[IW][(di_obb(IP, BI) / 4 + 1 + 3) & ~3u];
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
   uint32_t claimed;               // tasks of the workgroup's range claimed so far
@@ -1838,8 +1865,50 @@ struct DIShared {  // k_decode_items
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
   __device__ __forceinline__ uint32_t count() const { return 0; }
   __device__ __forceinline__ void put_nf(uint32_t, uint32_t) {}
+  __device__ __forceinline__ void put2(uint32_t, uint32_t) {}
   __device__ __forceinline__ void put(uint32_t, uint32_t) {}
   __device__ __forceinline__ void flush() {}
+};
+
+// The item decoder's sink (DD_ACC): the lane's pending output bytes in a
+// register word `lo` (na bits, < 32), written whole to the lane's LDS
+// region with one ds_write_b32 per fast pair (up to four symbols) instead of
+// two ds_write_b8 per step -- the pair loop is LDS-issue heavy (two gathered
+// lookups, the input word, and before this four byte stores per pair).  The
+// word is written at every put, so the region always holds the bytes so far
+// (the bytes past count() are don't-care); a put that fills the word moves
+// on to the next one with the bits that overflowed it.
+struct LdsAccSink {
+  lds_u32 *p, *base;
+  uint32_t lo, na;
+  __device__ __forceinline__ LdsAccSink(lds_u8 *b) : p((lds_u32 *)b), base((lds_u32 *)b), lo(0), na(0) {}
+  __device__ __forceinline__ uint32_t count() const { return 4u * (uint32_t)(p - base) + (na >> 3); }
+  // the two lookup entries of a fast pair (sym1 | sym2 << 8, 8 cnt at bits 16..20)
+  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
+    const uint32_t c1 = E_CNT8(e1), c2 = E_CNT8(e2);
+    const uint32_t v = ((e2 & 0xFFFFu) << c1) | (e1 & 0xFFFFu);  // <= 32 bits
+    const uint64_t t = (uint64_t)v << na;
+    lo |= (uint32_t)t;
+    *p = lo;
+    na += c1 + c2;
+    const bool sp = na >= 32u;
+    lo = sp ? (uint32_t)(t >> 32) : lo;
+    p += sp ? 1 : 0;
+    na &= 31u;
+  }
+  // one step's symbols: v holds c8 / 8 (0..2) bytes, nothing above them
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) {
+    const uint64_t t = (uint64_t)v << na;
+    lo |= (uint32_t)t;
+    *p = lo;
+    na += c8;
+    const bool sp = na >= 32u;
+    lo = sp ? (uint32_t)(t >> 32) : lo;
+    p += sp ? 1 : 0;
+    na &= 31u;
+  }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) { put(v & 0xFFFFu, c8); }
+  __device__ __forceinline__ void flush() { *p = lo; }
 };
 
 struct LdsSink {
@@ -1856,6 +1925,10 @@ struct LdsSink {
     }
     n += c8 >> 3;
   }
+  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
+    put_nf(e1 & 0xFFFFu, E_CNT8(e1));
+    put_nf(e2 & 0xFFFFu, E_CNT8(e2));
+  }
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
   __device__ __forceinline__ void flush() {}
 };
@@ -1864,15 +1937,21 @@ struct LdsSink {
 // than base + count).
 struct LdsPtrSink {
   lds_u8 *p, *base;
+  __device__ __forceinline__ LdsPtrSink(lds_u8 *b) : p(b), base(b) {}
   __device__ __forceinline__ uint32_t count() const { return (uint32_t)(p - base); }
   __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
     p[0] = (uint8_t)v;
     p[1] = (uint8_t)(v >> 8);
     p += c8 >> 3;
   }
+  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
+    put_nf(e1 & 0xFFFFu, E_CNT8(e1));
+    put_nf(e2 & 0xFFFFu, E_CNT8(e2));
+  }
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
   __device__ __forceinline__ void flush() {}
 };
+typedef std::conditional<DD_ACC != 0, LdsAccSink, LdsPtrSink>::type DISink;
 
 // Staged input, skewed: logical dword k lives at k + k / 8, and each block of
 // 8 is followed by a copy of the next block's first dword, so the two dwords
@@ -1935,7 +2014,45 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   r.t = 0;
   r.win = 0;
   bool failed = false;
-  int32_t G2 = min((int32_t)bstop - 27, (int32_t)bend - 28);  // last start of a fast pair
+  // last start of a fast pair: every code it takes starts before bstop (the
+  // second step's second symbol at most LB + (LB - 5) bits on) and ends
+  // inside the string (two steps take at most 2 LB bits)
+  int32_t G2 = DD_G2OLD ? min((int32_t)bstop - 27, (int32_t)bend - 28)
+                        : min((int32_t)bstop - (2 * TT::BITS - 4), (int32_t)bend - 2 * TT::BITS);
+  if (DD_WIN) {
+    // fast pairs from a 32-bit window read at each pair's start (two staged
+    // words and one v_alignbit: q = bp - 1, the window is {w[q/32],
+    // w[q/32+1]} >> (~q & 31)) instead of a refilled 64-bit register buffer:
+    // fewer VALU per pair, one more LDS read on the pair's chain
+    uint32_t q = bp - 1u;
+    const int32_t Gq = G2 - 1;
+    while ((int32_t)q <= Gq) {
+      DCTR(0);
+      const uint32_t kq = q >> 5;
+      const uint32_t win = __builtin_amdgcn_alignbit(ib(kq), ib(kq + 1u), ~q);
+      const uint32_t e1 = T.lut[win >> (32 - TT::BITS)];
+      const uint32_t U1 = E_USED(e1);
+      const uint32_t e2 = T.lut[(win << U1) >> (32 - TT::BITS)];
+      sink.put2(e1, e2);
+      q += U1 + E_USED(e2);
+      if (e2 == 0u) {  // a code longer than the lookup at q + 1 (an e1 of 0 stalls e2 too)
+        const uint32_t kq2 = q >> 5;
+        const uint32_t w = __builtin_amdgcn_alignbit(ib(kq2), ib(kq2 + 1u), ~q);
+        const uint32_t rem_ = bend - (q + 1u);
+        const uint32_t e_ = slow_entry(T, w, rem_);
+        if (e_ == 0xFFFFFFFFu) {
+          failed = true;
+          break;
+        } else if (E_L1(e_) > rem_) {
+          break;  // the string's tail: the careful steps find it again
+        }
+        sink.put(e_ & 0xFFFFu, E_CNT8(e_));
+        q += E_USED(e_);
+      }
+    }
+    bp = q + 1u;
+    G2 = INT32_MIN;  // (the register-buffer loop below does not run)
+  }
   uint32_t k = bp >> 5;
   const uint32_t o = bp & 31u;
   const uint32_t w0 = ib(k), w1 = ib(k + 1u);
@@ -1967,17 +2084,22 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   while ((int32_t)bp <= G2) {
     DCTR(0);
     const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
-    sink.put_nf(e1 & 0xFFFFu, E_CNT8(e1));
     const uint32_t U1 = E_USED(e1);
     bb <<= U1;
     const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
-    sink.put_nf(e2 & 0xFFFFu, E_CNT8(e2));
+    sink.put2(e1, e2);
     const uint32_t U2 = E_USED(e2);
     bb <<= U2;
     bp += U1 + U2;
     nb -= U1 + U2;
     DD_REFILL();
-    if (e2 == 0u) DD_SLOW();  // (an e1 of 0 stalls e2 too)
+    if (DD_SLOWU) {  // the rare long code behind one uniform branch
+      if (__ballot(e2 == 0u)) {
+        if (e2 == 0u) DD_SLOW();
+      }
+    } else if (e2 == 0u) {
+      DD_SLOW();  // (an e1 of 0 stalls e2 too)
+    }
   }
 #undef DD_SLOW
   WSTAMP(10);
@@ -2020,7 +2142,9 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     // behind one uniform branch
     while (__ballot(!done)) {
       DCTR(2);
-      const uint32_t w = (uint32_t)(bb >> 32);
+      // (DD_WINC: the step's window read from the staged words at bp)
+      const uint32_t w = DD_WINC ? __builtin_amdgcn_alignbit(ib((bp - 1u) >> 5), ib(((bp - 1u) >> 5) + 1u), ~(bp - 1u))
+                                 : (uint32_t)(bb >> 32);
       const uint32_t rem = bend - bp;
       const bool stop = done || bp >= bstop || rem == 0u;
       uint32_t e = T.lut[w >> (32 - TT::BITS)];
@@ -2037,11 +2161,13 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       r.t = tail ? rem : r.t;
       r.win = tail ? w : r.win;
       const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
-      sink.put(take2 ? (e & 0xFFFFu) : (e & 0xFFu), take2 ? 16u : (take1 ? 8u : 0u));
-      bb <<= adv;
+      sink.put(take2 ? (e & 0xFFFFu) : (take1 ? (e & 0xFFu) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
       bp += adv;
-      nb -= adv;
-      DD_REFILL();
+      if (!DD_WINC) {
+        bb <<= adv;
+        nb -= adv;
+        DD_REFILL();
+      }
       failed = failed || eos;
       done = done || eos || !take1 || bp >= bstop;
     }
@@ -2067,7 +2193,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
           r.win = w;
         }
         const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
-        sink.put(take2 ? (e & 0xFFFFu) : (e & 0xFFu), take2 ? 16u : (take1 ? 8u : 0u));
+        sink.put(take2 ? (e & 0xFFFFu) : (take1 ? (e & 0xFFu) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
         bb <<= adv;
         bp += adv;
         nb -= adv;
@@ -2077,6 +2203,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     }
   }
   WSTAMP(11);
+  sink.flush();
   if (!failed && bp == bend) r.at_end = true;
   r.failed = failed;
   WSTAMP(12);
@@ -2415,7 +2542,7 @@ __global__ __launch_bounds__(DD_NT) void k_decode_dense(const uint8_t *__restric
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
-template <uint32_t IP, int IW, int LB>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
 __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
                                                         const uint32_t *__restrict__ off,
                                                         uint32_t n, uint8_t *__restrict__ dst,
@@ -2424,10 +2551,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
                                                         int32_t *__restrict__ status,
                                                         uint16_t *__restrict__ fstate_out,
                                                         uint8_t *__restrict__ flags_out) {
-  __shared__ DIShared<IP, IW, LB> S;
+  __shared__ DIShared<IP, IW, LB, BI> S;
+  constexpr uint32_t kSpan = di_span(IP, BI), kPF = di_pf(kSpan);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   lds_u32 *ibw = (lds_u32 *)S.ib[wv];
   const lds_u32 *ibe = ibw;
+  // (budgeted rounds: the lane's output region moves with the round)
   lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
   lds_u32 *ost = (lds_u32 *)S.ostart[wv];
@@ -2484,15 +2613,15 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     if (lane == 0) v = atomicAdd((uint32_t *)&S.claimed, 1u);
     return t_lo + IW + __builtin_amdgcn_readfirstlane(v);
   };
-  // a task's string offsets are loaded one task ahead, and the first round
-  // of the next task is staged into registers during the current task's last
-  // round (pf), so neither waits at a task start
-  uint32_t na_l = 0, nb_l = 0;
-  auto load_offs = [&](uint32_t tk) {
+  // a task's string offsets are loaded one task ahead (DD_LATE: two), and
+  // the first round of the next task is staged into registers during the
+  // current task's last round (pf), so neither waits at a task start
+  uint32_t na_l = 0, nb_l = 0, n2a_l = 0, n2b_l = 0;
+  auto load_offs = [&](uint32_t tk, uint32_t &xa, uint32_t &xb) {
     const uint32_t u0 = tk * TASK_STR;
     const bool in = tk < ntask && lane < min(n - u0, (uint32_t)TASK_STR);
-    na_l = in ? off[u0 + lane] : 0u;
-    nb_l = in ? off[u0 + lane + 1] : 0u;
+    xa = in ? off[u0 + lane] : 0u;
+    xb = in ? off[u0 + lane + 1] : 0u;
   };
   // the staged range of a round whose items start at byte R0 (a round's
   // items are contiguous in the pool, the next one starting where the last
@@ -2500,22 +2629,49 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   // (clipped to the task [A, Z), aligned)
   auto round_range = [&](uint32_t R0, uint32_t A, uint32_t Z, uint32_t &IBo, uint32_t &nchunk) {
     IBo = (R0 - A > DD_OV ? R0 - DD_OV : A) & ~15u;
-    nchunk = (((min(R0 + WAVE * IP, Z) + 8u + 15u) & ~15u) - IBo) >> 4;
+    nchunk = (((min(R0 + kSpan, Z) + 8u + 15u) & ~15u) - IBo) >> 4;
   };
-  uint4 pf[di_pf(IP)];
-  uint32_t pf_IB = 0xFFFFFFFFu;
-  load_offs(t_first < t_hi ? t_first : ntask);
-  uint32_t next_task = t_hi;
-  for (uint32_t task = t_first; task < t_hi; task = next_task) {
-    next_task = claim_next(task);
+  // DD_LATE: vmcnt counts loads and stores together and in order, so a wait
+  // for loads issued after a round's output stores waits for those stores
+  // too.  The prefetched input of the next round is therefore written to the
+  // staging buffer at the END of the current round (after its verify, before
+  // its status and output stores), and the string offsets are loaded two
+  // tasks ahead and moved along at the end of a task (after that wait): every
+  // wait then falls a whole round after the last stores.
+  constexpr bool kLate = DD_LATE && !DD_GIN;
+  uint4 pf[kPF];
+  uint32_t pf_IB = 0xFFFFFFFFu, pf_n = 0, staged_IB = 0xFFFFFFFFu;
+  uint32_t ca_l = 0, cb_l = 0;  // kLate: the current task's offsets
+  load_offs(t_first < t_hi ? t_first : ntask, kLate ? ca_l : na_l, kLate ? cb_l : nb_l);
+  uint32_t next_task = t_hi, next2 = t_hi;
+  if (kLate) {
+    next_task = t_first < t_hi ? claim_next(t_first) : t_hi;
+    load_offs(next_task < t_hi ? next_task : ntask, na_l, nb_l);
+    next2 = next_task < t_hi ? claim_next(next_task) : t_hi;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (the loop's first wait-free copies)
+  }
+  // kLate: the next task becomes the current one, the one after it the next
+  // (after a round's wait; the offsets of the task after those are loaded at
+  // the top of the task, so no register copy at the loop latch waits for them)
+  auto rotate = [&]() {
+    ca_l = na_l;
+    cb_l = nb_l;
+    na_l = n2a_l;
+    nb_l = n2b_l;
+    next_task = next2;
+    next2 = next2 < t_hi ? claim_next(next2) : t_hi;
+  };
+  for (uint32_t task = t_first; task < t_hi;) {
+    if (kLate) load_offs(next2 < t_hi ? next2 : ntask, n2a_l, n2b_l);
+    else next_task = claim_next(task);
     WCOUNT(8);
     const uint32_t t0 = task * TASK_STR;
     const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
     const bool sl = lane < nstr;
-    const uint32_t a_l = na_l, b_l = nb_l;
+    const uint32_t a_l = kLate ? ca_l : na_l, b_l = kLate ? cb_l : nb_l;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
-    load_offs(next_task < t_hi ? next_task : ntask);
+    if (!kLate) load_offs(next_task < t_hi ? next_task : ntask, na_l, nb_l);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
     if (__ballot(sl && (b_l < a_l || a_l < off0))) {
@@ -2525,6 +2681,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         status[t0 + lane] = NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
         dst_off[t0 + lane] = (uint32_t)min(tbase, dst_cap);
         if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase, dst_cap);
+      }
+      staged_IB = 0xFFFFFFFFu;  // (staged for this task's first round)
+      task = next_task;
+      if (kLate) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // (as at a round's end)
+        rotate();
       }
       continue;
     }
@@ -2536,10 +2698,9 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     uint32_t ocarry = 0;  // the partial last output word of the round before
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
-    for (uint32_t r0 = 0; r0 < M; r0 += WAVE) {
-      const uint32_t nv = min(M - r0, (uint32_t)WAVE);
+    for (uint32_t r0 = 0, nv = 0; r0 < M; r0 += nv) {
+      nv = min(M - r0, (uint32_t)WAVE);  // (budgeted rounds: cut below)
       const uint32_t q = r0 + lane;
-      const bool valid = lane < nv;
       // this lane's item: its string i = the last one with X_i <= q; every
       // string with an item in the round marks its first one (or item 0 of
       // the round), then a max-scan over the lanes
@@ -2558,8 +2719,24 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         k = q - __shfl(X_l, i, 64);
         a = __shfl(a_l, i, 64);
         b = __shfl(b_l, i, 64);
+      } else if (BI && r0) {  // (a budgeted round after the first: item q = string q)
+        i = min(q, nstr - 1u);
+        a = __shfl(a_l, i, 64);
+        b = __shfl(b_l, i, 64);
       }
       const uint32_t s = a + IP * k, e = min(b, s + IP);
+      if (BI) {
+        // budgeted round: the items of the next 64 that fit BI input bytes
+        // (the first always does: IP <= BI), each lane's output region right
+        // after the one before (no region crosses the round's di_obb bytes)
+        const uint32_t x = lane < nv ? e - s : 0u;
+        const uint32_t cx = wave_incl_scan(x);
+        nv = (uint32_t)__builtin_popcountll(__ballot(lane < nv && cx <= BI));
+        const uint32_t rb = lane < nv ? di_rb(x) : 0u;
+        my_ob = (lds_u8 *)S.ob[wv] + (wave_incl_scan(rb) - rb);
+        my_ob32 = (const lds_u32 *)my_ob;
+      }
+      const bool valid = lane < nv;
       const bool last = e == b;
       const bool spec = valid && k > 0;
       WCOUNT(9);
@@ -2573,17 +2750,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
 #else
       const LdsIn inp{ibe};
 #endif
-      if (!DD_GIN) {
-        const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
-        if (pf_IB != IB) {  // (not prefetched)
+      // the prefetched chunks (pf) into the staging buffer, byte-swapped
+      auto stage_pf = [&](uint32_t nch) {
 #pragma unroll
-          for (uint32_t u = 0; u < di_pf(IP); ++u)
-            if (lane + WAVE * u < nchunk) pf[u] = g[lane + WAVE * u];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < di_pf(IP); ++u) {
+        for (uint32_t u = 0; u < kPF; ++u) {
           const uint32_t c = lane + WAVE * u;
-          if (c < nchunk) {
+          if (c < nch) {
             u32x4 v;
             v.x = __builtin_bswap32(pf[u].x);
             v.y = __builtin_bswap32(pf[u].y);
@@ -2595,11 +2767,23 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      };
+      if (!DD_GIN) {
+        // (kLate: only a round that the round before did not stage)
+        if (!kLate || staged_IB != IB) {
+          const uint4 *g = reinterpret_cast<const uint4 *>(src + IB);
+          if (pf_IB != IB) {  // (not prefetched)
+#pragma unroll
+            for (uint32_t u = 0; u < kPF; ++u)
+              if (lane + WAVE * u < nchunk) pf[u] = g[lane + WAVE * u];
+          }
+          stage_pf(nchunk);
+        }
         // prefetch the next round: of this task, else the next task's first
         pf_IB = 0xFFFFFFFFu;
         uint32_t IBn = 0, ncn = 0;
-        if (r0 + WAVE < M) {
-          round_range(__builtin_amdgcn_readlane(e, WAVE - 1u), A, Z, IBn, ncn);
+        if (r0 + nv < M) {
+          round_range(__builtin_amdgcn_readlane(e, nv - 1u), A, Z, IBn, ncn);
           pf_IB = IBn;
         } else if (next_task < t_hi) {
           const uint32_t An = __builtin_amdgcn_readfirstlane(na_l);
@@ -2611,9 +2795,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         if (pf_IB != 0xFFFFFFFFu) {
           const uint4 *gn = reinterpret_cast<const uint4 *>(src + IBn);
 #pragma unroll
-          for (uint32_t u = 0; u < di_pf(IP); ++u)
+          for (uint32_t u = 0; u < kPF; ++u)
             if (lane + WAVE * u < ncn) pf[u] = gn[lane + WAVE * u];
         }
+        pf_n = ncn;
       }
       WSTAMP(1);
       if (carry_exit < DD_NONE) carry_exit -= 8u * (IB - IB_prev);
@@ -2621,7 +2806,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t bs = 8u * (s - IBX);
       const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
       const uint32_t bstop = last ? bend : 8u * (e - IBX);
-      LdsPtrSink sk{my_ob, my_ob};
+      DISink sk(my_ob);
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
@@ -2653,7 +2838,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         DCTR(3);
         const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
         if (mism && !pred_mism) {
-          LdsPtrSink s3{my_ob, my_ob};
+          DISink s3(my_ob);
           if (pred == XFAIL || pred == XUNKNOWN || pred == DD_NONE) {
             rr.failed = true;  // the string failed in an earlier item
             rr.at_end = false;
@@ -2677,6 +2862,14 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t h1 = wave_incl_max((!valid || k == 0) ? lane + 1u : 0u);
       const uint32_t excl_h = __shfl(Tinc - V, h1 ? h1 - 1u : 0u, 64);
       const uint32_t seg = h1 ? Tinc - excl_h : Tinc + carry_cnt;  // inclusive
+      if (kLate) {  // the staging buffer is free: the next round's input into it
+        staged_IB = pf_IB;
+        if (pf_IB != 0xFFFFFFFFu) stage_pf(pf_n);
+        // every load of the wave has landed (the offsets two tasks ahead
+        // included): said explicitly, so no wait for them is placed after
+        // this round's stores (vmcnt(0): expcnt and lgkmcnt left at max)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
       if (valid && last)
         dd_finish(S.T, rr.failed, rr.t, rr.win, seg,
                   task_ovf && auto_slot(b - off0, t0 + i + 1u) > dst_cap, t0 + i, status,
@@ -2741,7 +2934,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const bool lastr = r0 + WAVE >= M;
+        const bool lastr = r0 + nv >= M;
         const uint32_t nst = lastr ? nwr : (uint32_t)((R1g >> 2) - W0);
         for (uint32_t i4 = 4u * lane; i4 < nst; i4 += 4u * WAVE) {
           const uint64_t gq = 4ull * (W0 + i4);
@@ -2819,6 +3012,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    task = next_task;
+    if (kLate) rotate();
   }
   WSTAMP_FLUSH_W(IW);
 }
@@ -3020,23 +3215,26 @@ extern "C" __attribute__((visibility("default"))) int nghttp2_amd_hd__diag_stamp
 }
 #endif
 
-template <uint32_t IP, int IW, int LB>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
 static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
                                 uint8_t *dst, size_t dst_cap, uint32_t *dst_off,
                                 int32_t *status, uint16_t *fstate, uint8_t *flags,
                                 hipStream_t st) {
-  hipLaunchKernelGGL((k_decode_items<IP, IW, LB>),
-                     dim3(persistent_grid<k_decode_items<IP, IW, LB>, WAVE * IW, TASK_STR * IW>(n)),
+  hipLaunchKernelGGL((k_decode_items<IP, IW, LB, BI>),
+                     dim3(persistent_grid<k_decode_items<IP, IW, LB, BI>, WAVE * IW, TASK_STR * IW>(n)),
                      dim3(WAVE * IW), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off,
                      status, fstate, flags);
 }
 
-// piece = 64 / 40 / 32 picks an instance; 0 picks by the batch's mean
-// encoded string length, estimated from the pool size (dst_cap is normally
-// nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 + 4 n), so that most
-// strings are one item.  Header strings of up to ~48 bytes fit whole 64-byte
-// items: no warm-up or item map, and the 14-bit lookup (most two-symbol
-// steps) at 8 waves per CU.  Shorter ones (mean <= 20 bytes) fit 32-byte
+// piece = 64 / 40 / 32 (66..69: budgeted rounds) picks an instance; 0 picks
+// by the batch's mean encoded string length, estimated from the pool size
+// (dst_cap is normally nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 +
+// 4 n), so that most strings are one item.  Header strings of up to ~48
+// bytes fit whole 64-byte items (no warm-up or item map) in budgeted rounds
+// of at most 2048 input bytes, whose staging and output regions are sized
+// for that budget instead of 64 full items: 16 waves per CU with the 13-bit
+// lookup (config 2: 59.7 us, against 70.4 for <64, 8, 14> without a budget
+// and 62.8 for the 14-bit lookup at 12 waves).  Shorter ones (mean <= 20 bytes) fit 32-byte
 // items, and longer values are cut into 40-byte pieces; both decode with
 // the 13-bit lookup, whose 32 KB less LDS buys 16 waves per CU (measured:
 // config 3 360 vs 385 us for 40-byte items with the 14-bit lookup at 12
@@ -3053,12 +3251,16 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (piece == 0) {
     const uint64_t est =
         (uint64_t)dst_cap > 4ull * n ? ((uint64_t)dst_cap - 4ull * n) * 5u / 8u : 0u;
-    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 64 : 40;
+    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 67 : 40;
   }
-#define DI_LAUNCH(P, W, B) \
-  launch_decode_items<P, W, B>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st)
+#define DI_LAUNCH(P, W, B, ...) \
+  launch_decode_items<P, W, B, ##__VA_ARGS__>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st)
   switch (piece) {
     case 64: DI_LAUNCH(64u, 8, 14); break;
+    case 66: DI_LAUNCH(64u, 12, 14, 2048u); break;  // budgeted rounds
+    case 67: DI_LAUNCH(64u, 16, 13, 2048u); break;
+    case 68: DI_LAUNCH(64u, 16, 13, 2304u); break;
+    case 69: DI_LAUNCH(32u, 16, 14, 1280u); break;
     case 40: DI_LAUNCH(40u, 16, 13); break;
     case 32: DI_LAUNCH(32u, 16, 13); break;
 #if DD_XINST  // A/B builds: the other lookup width at the same pieces

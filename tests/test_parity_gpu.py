@@ -250,7 +250,7 @@ def _variant_inputs():
     yield "mixed", e3, eo3
 
 
-@pytest.mark.parametrize("variant", ["auto", "items64", "items40", "items32", "fsm"])
+@pytest.mark.parametrize("variant", ["auto", "items64", "items66", "items67", "items68", "items69", "items40", "items32", "fsm"])
 def test_decode_variants_match_oracle(codec, dev, variant):
     """decode_batch_auto (dense item decoder: the library's pick and every
     instance) and the batched reference FSM kernel agree with the oracle on
@@ -382,7 +382,7 @@ def test_emit_strings_parity(codec, dev, kind):
     check_emit(codec, dev, pool, off, kind)
 
 
-@pytest.mark.parametrize("piece", [0, 64, 40, 32])
+@pytest.mark.parametrize("piece", [0, 64, 66, 67, 68, 69, 40, 32])
 def test_dense_decode_edges(codec, dev, piece):
     """decode_batch_auto (each item-decoder instance) on strings that stress
     its pieces:

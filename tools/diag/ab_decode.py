@@ -35,7 +35,7 @@ def main():
     kern = {"dense": L0.nghttp2_amd_hd_huff_decode_batch_auto,
             "slots_r1": L0.nghttp2_amd_hd__decode_batch_slots,
             "pieces": L0.nghttp2_amd_hd__decode_batch_pieces}
-    for pc in (64, 40, 32):
+    for pc in (64, 66, 67, 68, 69, 40, 32):
         kern["items%d" % pc] = (lambda pc: lambda *a: L0.nghttp2_amd_hd__decode_batch_items(*a, pc))(pc)
     for p in sorted(glob.glob(os.path.join(HERE, "lib_x*.so"))):  # extra instances (DD_XINST builds)
         Lx = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
@@ -84,12 +84,18 @@ def main():
                 run(k)
         torch.cuda.synchronize()
         ref = bufs["dense"]
-        for k in kern:
+        for k in list(kern):
             if k.startswith("abl"):
                 continue  # ablation builds give wrong output on purpose
-            assert torch.equal(bufs[k][2], ref[2]), k + ": status differs"
-            if k not in ("slots_r1", "pieces"):
-                assert torch.equal(bufs[k][1], ref[1]) and torch.equal(bufs[k][0], ref[0]), k
+            bad = not torch.equal(bufs[k][2], ref[2])
+            if not bad and k not in ("slots_r1", "pieces"):
+                bad = not (torch.equal(bufs[k][1], ref[1]) and torch.equal(bufs[k][0], ref[0]))
+            if bad:  # report (first differing strings) and leave the variant out
+                d = (bufs[k][2] != ref[2]).nonzero().flatten()[:8].tolist()
+                print(json.dumps({"config": cfg, "variant": k, "MISMATCH": True, "status_idx": d,
+                                  "ref": [int(ref[2][i]) for i in d],
+                                  "got": [int(bufs[k][2][i]) for i in d]}), flush=True)
+                del kern[k]
         res = {k: [] for k in kern}
         for _ in range(10):
             for k in kern:
