@@ -16,9 +16,11 @@
 //                   into pairs and quads in registers and OR'ed into an LDS
 //                   image that leaves as whole big-endian dwords
 //   k_decode_items  decode_batch_auto: persistent waves, tasks of 64 strings,
-//                   rounds of 64 items (a string, or a 40/64-byte piece of a
-//                   long one, warmed up and verified); a 14-bit two-symbol
-//                   lookup in LDS and a register bit buffer; symbols through
+//                   rounds of up to 64 items (a string, or a 32/40/64-byte
+//                   piece of a long one, warmed up and verified; budgeted
+//                   instances cut a round at an input-byte budget); a 13- or
+//                   14-bit two-symbol lookup in LDS and a register bit
+//                   buffer; symbols through
 //                   a per-lane LDS region, stored back to back per task; the
 //                   final {fstate, flags} of the reference's nibble FSM
 //                   (lib/nghttp2_hd_huffman.c:122-136) rebuilt exactly from
@@ -1801,6 +1803,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_LATE
 #define DD_LATE 0  // item decoder: the next round's input staged at the end of a round (see kLate)
 #endif
+#ifndef DD_ST4
+#define DD_ST4 0  // item decoder, realigned stores: four whole dwords as one 16-byte store
+#endif
 #ifndef DD_G2OLD
 #define DD_G2OLD 0  // A/B builds: the round-2 fast-pair bound (bstop - 27, bend - 28)
 #endif
@@ -2972,11 +2977,16 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           uint32_t c[4];
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) c[j] = m0 + j < di_rb(IP) / 4 ? my_ob32[m0 + j + 1u] : 0u;
+          uint32_t v[4];
 #pragma unroll
-          for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t m = m0 + j;
-            const uint32_t v = __builtin_amdgcn_alignbyte(c[j], j ? c[j - 1] : prev, h);
-            if (m < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * m) = v;
+          for (uint32_t j = 0; j < 4; ++j) v[j] = __builtin_amdgcn_alignbyte(c[j], j ? c[j - 1] : prev, h);
+          if (DD_ST4 && m0 + 4u <= nfull && fits) {
+            // four whole dwords as one (dword-aligned) 16-byte store
+            *reinterpret_cast<uint4 *>(dst + g0 + h + 4u * m0) = make_uint4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+              if (m0 + j < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * (m0 + j)) = v[j];
           }
           prev = c[3];
         }
@@ -3231,12 +3241,14 @@ static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uin
 // (dst_cap is normally nghttp2_amd_hd_huff_decode_bound(E, n) = 8 E / 5 +
 // 4 n), so that most strings are one item.  Header strings of up to ~48
 // bytes fit whole 64-byte items (no warm-up or item map) in budgeted rounds
-// of at most 2048 input bytes, whose staging and output regions are sized
+// of at most 2304 input bytes, whose staging and output regions are sized
 // for that budget instead of 64 full items: 16 waves per CU with the 13-bit
-// lookup (config 2: 59.7 us, against 70.4 for <64, 8, 14> without a budget
-// and 62.8 for the 14-bit lookup at 12 waves).  Shorter ones (mean <= 20 bytes) fit 32-byte
-// items, and longer values are cut into 40-byte pieces; both decode with
-// the 13-bit lookup, whose 32 KB less LDS buys 16 waves per CU (measured:
+// lookup (config 2: 56.0 us, against 71-72 for <64, 8, 14> without a budget,
+// 59.7 with a 2048-byte budget (2.3 % of config 2's tasks take two rounds),
+// 55.7 / 56.7 with 2432 / 2560, 62.8 for the 14-bit lookup at 12 waves).
+// Shorter ones (mean <= 20 bytes) fit 32-byte items, and longer values are
+// cut into 40-byte pieces; both decode with the 13-bit lookup, whose 32 KB
+// less LDS buys 16 waves per CU (measured:
 // config 3 360 vs 385 us for 40-byte items with the 14-bit lookup at 12
 // waves; the adversarial config 5 162 us in 32-byte items vs 261 in 64-byte
 // ones).  Every instance writes the same layout.
@@ -3251,7 +3263,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (piece == 0) {
     const uint64_t est =
         (uint64_t)dst_cap > 4ull * n ? ((uint64_t)dst_cap - 4ull * n) * 5u / 8u : 0u;
-    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 67 : 40;
+    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 68 : 40;
   }
 #define DI_LAUNCH(P, W, B, ...) \
   launch_decode_items<P, W, B, ##__VA_ARGS__>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st)
@@ -3263,7 +3275,9 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
     case 69: DI_LAUNCH(32u, 16, 14, 1280u); break;
     case 40: DI_LAUNCH(40u, 16, 13); break;
     case 32: DI_LAUNCH(32u, 16, 13); break;
-#if DD_XINST  // A/B builds: the other lookup width at the same pieces
+#if DD_XINST  // A/B builds: the other lookup width at the same pieces; other budgets
+    case 70: DI_LAUNCH(64u, 16, 13, 2560u); break;
+    case 71: DI_LAUNCH(64u, 16, 13, 2432u); break;
     case 65: DI_LAUNCH(64u, 10, 13); break;
     case 41: DI_LAUNCH(40u, 12, 14); break;
     case 44: DI_LAUNCH(44u, 15, 13); break;

@@ -235,7 +235,8 @@ class HuffmanBatchCodec:
         """Decode into a dense pool (one launch): the strings of each task of
         64 consecutive strings back to back from the task's base
         auto_slot(x_t0, t0).  piece = 64 / 40 / 32 forces an instance of the
-        item decoder (tests, A/B); 0 lets the library pick.  Returns
+        item decoder, 66..69 a budgeted-round instance (tests, A/B); 0 lets
+        the library pick.  Returns
         (dst, dst_off, status[, fstate, flags])."""
         torch = self.torch
         n = src_off.numel() - 1

@@ -35,7 +35,7 @@ def main():
     kern = {"dense": L0.nghttp2_amd_hd_huff_decode_batch_auto,
             "slots_r1": L0.nghttp2_amd_hd__decode_batch_slots,
             "pieces": L0.nghttp2_amd_hd__decode_batch_pieces}
-    for pc in (64, 66, 67, 68, 69, 40, 32):
+    for pc in (64, 67, 68, 70, 71, 40, 32):
         kern["items%d" % pc] = (lambda pc: lambda *a: L0.nghttp2_amd_hd__decode_batch_items(*a, pc))(pc)
     for p in sorted(glob.glob(os.path.join(HERE, "lib_x*.so"))):  # extra instances (DD_XINST builds)
         Lx = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
