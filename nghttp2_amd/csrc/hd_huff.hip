@@ -1758,7 +1758,7 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #define DD_P 32u   // piece bytes per lane
 #endif
 #ifndef DD_OV
-#define DD_OV 24u  // warm-up bytes of a later item
+#define DD_OV 20u  // warm-up bytes of a later item (24 before: 314.2 vs 306.5 us on config 3)
 #endif
 #ifndef DD_WAVES
 #define DD_WAVES 14  // waves per workgroup: one lookup table per CU
@@ -1804,7 +1804,19 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #define DD_LATE 0  // item decoder: the next round's input staged at the end of a round (see kLate)
 #endif
 #ifndef DD_ST4
-#define DD_ST4 0  // item decoder, realigned stores: four whole dwords as one 16-byte store
+#define DD_ST4 1  // item decoder, realigned stores: four whole dwords as one 16-byte store
+#endif
+#ifndef DD_NTL
+#define DD_NTL 0  // item decoder: the staged input read with nontemporal loads
+#endif
+#ifndef DD_NTS
+#define DD_NTS 0  // item decoder: 16-byte output stores nontemporal
+#endif
+#ifndef DD_PICK_LONG
+#define DD_PICK_LONG 40  // A/B builds: the instance decode_batch_auto picks for long strings
+#endif
+#ifndef DD_HT2
+#define DD_HT2 0  // item decoder, realigned stores: head and tail bytes as 2-byte stores
 #endif
 #ifndef DD_G2OLD
 #define DD_G2OLD 0  // A/B builds: the round-2 fast-pair bound (bstop - 27, bend - 28)
@@ -1957,6 +1969,30 @@ struct LdsPtrSink {
   __device__ __forceinline__ void flush() {}
 };
 typedef std::conditional<DD_ACC != 0, LdsAccSink, LdsPtrSink>::type DISink;
+
+// the item decoder's 16-byte input loads and output stores (read or written
+// once: optionally with the nontemporal hint)
+__device__ __forceinline__ uint4 dd_ld16(const uint4 *p) {
+  if (DD_NTL) {
+    uint4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+  }
+  return *p;
+}
+__device__ __forceinline__ void dd_st16(uint4 *p, uint4 v) {
+  if (DD_NTS) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+  } else {
+    *p = v;
+  }
+}
 
 // Staged input, skewed: logical dword k lives at k + k / 8, and each block of
 // 8 is followed by a copy of the next block's first dword, so the two dwords
@@ -2780,7 +2816,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           if (pf_IB != IB) {  // (not prefetched)
 #pragma unroll
             for (uint32_t u = 0; u < kPF; ++u)
-              if (lane + WAVE * u < nchunk) pf[u] = g[lane + WAVE * u];
+              if (lane + WAVE * u < nchunk) pf[u] = dd_ld16(g + lane + WAVE * u);
           }
           stage_pf(nchunk);
         }
@@ -2801,7 +2837,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           const uint4 *gn = reinterpret_cast<const uint4 *>(src + IBn);
 #pragma unroll
           for (uint32_t u = 0; u < kPF; ++u)
-            if (lane + WAVE * u < ncn) pf[u] = gn[lane + WAVE * u];
+            if (lane + WAVE * u < ncn) pf[u] = dd_ld16(gn + lane + WAVE * u);
         }
         pf_n = ncn;
       }
@@ -2982,7 +3018,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           for (uint32_t j = 0; j < 4; ++j) v[j] = __builtin_amdgcn_alignbyte(c[j], j ? c[j - 1] : prev, h);
           if (DD_ST4 && m0 + 4u <= nfull && fits) {
             // four whole dwords as one (dword-aligned) 16-byte store
-            *reinterpret_cast<uint4 *>(dst + g0 + h + 4u * m0) = make_uint4(v[0], v[1], v[2], v[3]);
+            dd_st16(reinterpret_cast<uint4 *>(dst + g0 + h + 4u * m0), make_uint4(v[0], v[1], v[2], v[3]));
           } else {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
@@ -2994,10 +3030,23 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           const uint32_t vt = __builtin_amdgcn_alignbyte(my_ob32[nfull + 1u], my_ob32[nfull], h);
           const uint32_t nh = min(h, V);
           const uint32_t xt = h + 4u * nfull, ntl = V > xt ? V - xt : 0u;
+          if (DD_HT2 && fits) {
+            // the head up to alignment and the tail after the last whole
+            // dword as (aligned) 2-byte stores plus at most one byte each
+            if (nh == h) {
+              if (h & 1u) dst[g0] = (uint8_t)d0;
+              if (h & 2u) *reinterpret_cast<uint16_t *>(dst + g0 + (h & 1u)) = (uint16_t)(d0 >> (8u * (h & 1u)));
+            } else {
+              for (uint32_t x = 0; x < nh; ++x) dst[g0 + x] = (uint8_t)(d0 >> (8u * x));
+            }
+            if (ntl & 2u) *reinterpret_cast<uint16_t *>(dst + g0 + xt) = (uint16_t)vt;
+            if (ntl & 1u) dst[g0 + xt + (ntl & 2u)] = (uint8_t)(vt >> (8u * (ntl & 2u)));
+          } else {
 #pragma unroll
-          for (uint32_t x = 0; x < 3u; ++x) {
-            if (x < nh && fits) dst[g0 + x] = (uint8_t)(d0 >> (8u * x));
-            if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
+            for (uint32_t x = 0; x < 3u; ++x) {
+              if (x < nh && fits) dst[g0 + x] = (uint8_t)(d0 >> (8u * x));
+              if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
+            }
           }
           if (!fits) {  // near dst_cap: byte by byte, nothing at or past it
             for (uint32_t x = 0; x < V; ++x)
@@ -3246,12 +3295,12 @@ static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uin
 // lookup (config 2: 56.0 us, against 71-72 for <64, 8, 14> without a budget,
 // 59.7 with a 2048-byte budget (2.3 % of config 2's tasks take two rounds),
 // 55.7 / 56.7 with 2432 / 2560, 62.8 for the 14-bit lookup at 12 waves).
-// Shorter ones (mean <= 20 bytes) fit 32-byte items, and longer values are
-// cut into 40-byte pieces; both decode with the 13-bit lookup, whose 32 KB
-// less LDS buys 16 waves per CU (measured:
-// config 3 360 vs 385 us for 40-byte items with the 14-bit lookup at 12
-// waves; the adversarial config 5 162 us in 32-byte items vs 261 in 64-byte
-// ones).  Every instance writes the same layout.
+// Shorter ones too (the adversarial config 5: 158.6 us, against 164.3 in
+// 32-byte items with the 20-byte warm-up; 261 in unbudgeted 64-byte items at
+// 8 waves).  Longer values are cut into 40-byte pieces, also with the 13-bit
+// lookup, whose 32 KB less LDS buys 16 waves per CU (measured: config 3 360
+// vs 385 us for 40-byte items with the 14-bit lookup at 12 waves).  Every
+// instance writes the same layout.
 static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n, uint8_t *dst,
                         size_t dst_cap, uint32_t *dst_off, int32_t *status, uint16_t *fstate,
                         uint8_t *flags, void *stream, int piece) {
@@ -3263,7 +3312,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (piece == 0) {
     const uint64_t est =
         (uint64_t)dst_cap > 4ull * n ? ((uint64_t)dst_cap - 4ull * n) * 5u / 8u : 0u;
-    piece = est <= 20ull * n ? 32 : est <= 48ull * n ? 68 : 40;
+    piece = est <= 48ull * n ? 68 : DD_PICK_LONG;
   }
 #define DI_LAUNCH(P, W, B, ...) \
   launch_decode_items<P, W, B, ##__VA_ARGS__>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st)
@@ -3275,6 +3324,11 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
     case 69: DI_LAUNCH(32u, 16, 14, 1280u); break;
     case 40: DI_LAUNCH(40u, 16, 13); break;
     case 32: DI_LAUNCH(32u, 16, 13); break;
+#if DD_PICK_LONG != 40  // A/B builds: 40-byte pieces at fewer waves (LDS left for other kernels)
+    case 42: DI_LAUNCH(40u, 12, 13); break;
+    case 43: DI_LAUNCH(40u, 13, 13); break;
+    case 45: DI_LAUNCH(40u, 14, 13); break;
+#endif
 #if DD_XINST  // A/B builds: the other lookup width at the same pieces; other budgets
     case 70: DI_LAUNCH(64u, 16, 13, 2560u); break;
     case 71: DI_LAUNCH(64u, 16, 13, 2432u); break;
