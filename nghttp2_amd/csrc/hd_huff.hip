@@ -1282,6 +1282,7 @@ struct NullSink {
   __device__ __forceinline__ uint32_t count() const { return n8 >> 3; }
   __device__ __forceinline__ void put(uint32_t, uint32_t c8) { n8 += c8; }
   __device__ __forceinline__ void put_nf(uint32_t, uint32_t c8) { n8 += c8; }
+  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) { n8 += E_CNT8(e1) + E_CNT8(e2); }
   __device__ __forceinline__ void flush() {}
 };
 // Caller slots (any alignment, capacity checked), dword stores: as
@@ -1815,6 +1816,12 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_PICK_LONG
 #define DD_PICK_LONG 40  // A/B builds: the instance decode_batch_auto picks for long strings
 #endif
+#ifndef DD_CKPT
+#define DD_CKPT 0  // item decoder: a missed warm-up entry re-decoded only up to a checkpoint
+#endif
+#ifndef DD_CKB
+#define DD_CKB 48  // checkpoint distance (bits past a later item's entry)
+#endif
 #ifndef DD_HT2
 #define DD_HT2 0  // item decoder, realigned stores: head and tail bytes as 2-byte stores
 #endif
@@ -1969,6 +1976,7 @@ struct LdsPtrSink {
   __device__ __forceinline__ void flush() {}
 };
 typedef std::conditional<DD_ACC != 0, LdsAccSink, LdsPtrSink>::type DISink;
+static_assert(!(DD_CKPT && DD_ACC), "the checkpoint fix-up assumes the byte sink");
 
 // the item decoder's 16-byte input loads and output stores (read or written
 // once: optionally with the nontemporal hint)
@@ -2044,10 +2052,13 @@ struct DDRun {
     k += t_ ? 1u : 0u;                                                   \
     nxt = ib(k);                                                         \
   } while (0)
-template <class Sink, bool SYNC = false, class TT, class IN>
+// PAIRS: only the fast pairs, none starting past `lim` (no careful steps):
+// bp stops at a codeword boundary on the way, for a caller that records it
+// and goes on with another dd_run.
+template <class Sink, bool SYNC = false, bool PAIRS = false, class TT, class IN>
 __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
-                                        uint32_t *dctr DD_SARGS) {
+                                        uint32_t *dctr DD_SARGS, int32_t lim = INT32_MAX) {
   (void)dctr;
   WSTAMP(2);  // (the caller's bookkeeping)
   DDRun r;
@@ -2060,6 +2071,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // inside the string (two steps take at most 2 LB bits)
   int32_t G2 = DD_G2OLD ? min((int32_t)bstop - 27, (int32_t)bend - 28)
                         : min((int32_t)bstop - (2 * TT::BITS - 4), (int32_t)bend - 2 * TT::BITS);
+  if (PAIRS) G2 = min(G2, lim);
   if (DD_WIN) {
     // fast pairs from a 32-bit window read at each pair's start (two staged
     // words and one v_alignbit: q = bp - 1, the window is {w[q/32],
@@ -2144,6 +2156,11 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   }
 #undef DD_SLOW
   WSTAMP(10);
+  if (PAIRS) {
+    sink.flush();
+    r.failed = failed;
+    return r;
+  }
   if (SYNC) {
     // a warm-up only needs the first codeword boundary >= bstop: single
     // steps that take a 2-symbol entry's second symbol only while the first
@@ -2864,7 +2881,25 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       DDRun rr;
       rr.failed = rr.at_end = false;
       rr.t = rr.win = 0;
-      if (valid && !dead) rr = dd_run(S.T, inp, bp, bstop, bend, sk, dctr DD_SPASS);
+      // (DD_CKPT) a codeword boundary on the speculative path of a later
+      // item, DD_CKB bits or so past its entry, and the symbols before it
+      uint32_t cp_pos = XUNKNOWN, cp_cnt = 0;
+      if (valid && !dead) {
+        if (DD_CKPT && spec) {
+          // the fast pairs up to the checkpoint, then the rest of the item
+          const DDRun ra = dd_run<DISink, false, true>(S.T, inp, bp, bstop, bend, sk,
+                                                       dctr DD_SPASS, (int32_t)(entry + DD_CKB));
+          if (ra.failed) {
+            rr.failed = true;  // EOS before the checkpoint
+          } else {
+            cp_pos = bp;
+            cp_cnt = sk.count();
+            rr = dd_run(S.T, inp, bp, bstop, bend, sk, dctr DD_SPASS);
+          }
+        } else {
+          rr = dd_run(S.T, inp, bp, bstop, bend, sk, dctr DD_SPASS);
+        }
+      }
       uint32_t my_exit = rr.failed ? XFAIL : bp;
       uint32_t my_entry = dead ? XUNKNOWN : entry;
       uint32_t c0 = sk.count();
@@ -2885,13 +2920,44 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             rr.at_end = false;
             rr.t = rr.win = 0;
             my_exit = XFAIL;
+            c0 = 0u;
           } else {
-            uint32_t bq = pred;
-            rr = dd_run(S.T, inp, bq, bstop, bend, s3, dctr DD_SPASS);
-            my_exit = rr.failed ? XFAIL : bq;
+            bool fixed = false;
+            if (DD_CKPT && cp_pos != XUNKNOWN && pred <= cp_pos) {
+              // the true path from pred usually meets the speculative one
+              // within a few symbols: if it reaches the checkpoint, the
+              // symbols from there on are right already -- count the true
+              // symbols before it, move the rest to follow them, write them
+              uint32_t bq = pred;
+              NullSink ns;
+              const DDRun rc = dd_run(S.T, inp, bq, cp_pos, bend, ns, dctr DD_SPASS);
+              if (!rc.failed && bq == cp_pos) {
+                const uint32_t m = ns.count(), L = c0 - cp_cnt;
+                lds_u8 *o = my_ob;
+                if (m > cp_cnt) {
+                  for (uint32_t j = L; j-- > 0;) o[m + j] = o[cp_cnt + j];
+                } else if (m < cp_cnt) {
+                  for (uint32_t j = 0; j < L; ++j) o[m + j] = o[cp_cnt + j];
+                }
+                // (a sink may write up to two bytes past its count)
+                const uint8_t k0 = o[m], k1 = o[m + 1u];
+                uint32_t bq2 = pred;
+                DISink s4(my_ob);
+                dd_run(S.T, inp, bq2, cp_pos, bend, s4, dctr DD_SPASS);
+                if (L > 0u) o[m] = k0;
+                if (L > 1u) o[m + 1u] = k1;
+                c0 = m + L;
+                fixed = true;  // (exit and tail: the speculative path's)
+              }
+            }
+            if (!fixed) {
+              uint32_t bq = pred;
+              rr = dd_run(S.T, inp, bq, bstop, bend, s3, dctr DD_SPASS);
+              my_exit = rr.failed ? XFAIL : bq;
+              c0 = s3.count();
+            }
           }
           my_entry = pred;
-          c0 = s3.count();
         }
       }
       WSTAMP(4);
