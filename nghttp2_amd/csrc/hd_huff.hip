@@ -1816,6 +1816,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_PICK_LONG
 #define DD_PICK_LONG 40  // A/B builds: the instance decode_batch_auto picks for long strings
 #endif
+#ifndef DD_MERGE
+#define DD_MERGE 1  // item decoder: the item's decode and its re-decodes share one inlined copy
+                    // (instances without a budget: those whose later pieces warm up)
+#endif
 #ifndef DD_CKPT
 #define DD_CKPT 0  // item decoder: a missed warm-up entry re-decoded only up to a checkpoint
 #endif
@@ -2884,7 +2888,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // (DD_CKPT) a codeword boundary on the speculative path of a later
       // item, DD_CKB bits or so past its entry, and the symbols before it
       uint32_t cp_pos = XUNKNOWN, cp_cnt = 0;
-      if (valid && !dead) {
+      constexpr bool kMerge = DD_MERGE && BI == 0;
+      if (valid && !dead && !kMerge) {  // (kMerge: in the verify loop's first pass)
         if (DD_CKPT && spec) {
           // the fast pairs up to the checkpoint, then the rest of the item
           const DDRun ra = dd_run<DISink, false, true>(S.T, inp, bp, bstop, bend, sk,
@@ -2905,7 +2910,21 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       uint32_t c0 = sk.count();
       WSTAMP(3);
       // ---- verify the later items against the previous item's exit
-      for (uint32_t iter = 0; iter <= WAVE; ++iter) {
+      // (DD_MERGE: one inlined decoder for the item and its re-decodes -- a
+      // pass decodes the lanes marked run_ from `start`, then verifies)
+      bool run_ = kMerge && valid && !dead;
+      uint32_t start = entry;
+      for (uint32_t iter = 0; iter <= WAVE + (kMerge ? 1u : 0u); ++iter) {
+        if (kMerge && __ballot(run_)) {
+          if (run_) {
+            DISink s3(my_ob);
+            uint32_t bq = start;
+            rr = dd_run(S.T, inp, bq, bstop, bend, s3, dctr DD_SPASS);
+            my_exit = rr.failed ? XFAIL : bq;
+            c0 = s3.count();
+          }
+          run_ = false;
+        }
         const uint32_t up = __shfl_up(my_exit, 1, 64);
         const uint32_t pred = lane ? up : carry_exit;
         const bool mism = spec && (my_entry != pred || my_entry == XUNKNOWN);
@@ -2921,6 +2940,9 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             rr.t = rr.win = 0;
             my_exit = XFAIL;
             c0 = 0u;
+          } else if (kMerge) {
+            start = pred;  // (re-decoded in the next pass)
+            run_ = true;
           } else {
             bool fixed = false;
             if (DD_CKPT && cp_pos != XUNKNOWN && pred <= cp_pos) {
