@@ -1816,6 +1816,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_PICK_LONG
 #define DD_PICK_LONG 40  // A/B builds: the instance decode_batch_auto picks for long strings
 #endif
+#ifndef DD_TAILPOST
+#define DD_TAILPOST 0  // careful steps: the tail's bits and window taken after the loop
+#endif
 #ifndef DD_MERGE
 #define DD_MERGE 1  // item decoder: the item's decode and its re-decodes share one inlined copy
                     // (instances without a budget: those whose later pieces warm up)
@@ -2220,8 +2223,10 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       const bool take2 = take1 && E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
       const bool tail = !stop && !eos && !take1;  // a proper prefix of a code
       r.at_end = r.at_end || tail;
-      r.t = tail ? rem : r.t;
-      r.win = tail ? w : r.win;
+      if (!DD_TAILPOST) {
+        r.t = tail ? rem : r.t;
+        r.win = tail ? w : r.win;
+      }
       const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
       sink.put(take2 ? (e & 0xFFFFu) : (take1 ? (e & 0xFFu) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
       bp += adv;
@@ -2263,6 +2268,12 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
         done = !take1 || bp >= bstop;
       }
     }
+  }
+  if (DD_TAILPOST && DD_CAREFUL2 && !DD_WINC && r.at_end) {
+    // the tail's bits and window, after the loop: a lane that met its tail
+    // took no step after it (the refills only add stream bits below them)
+    r.t = bend - bp;
+    r.win = (uint32_t)(bb >> 32);
   }
   WSTAMP(11);
   sink.flush();
