@@ -1819,6 +1819,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_TAILPOST
 #define DD_TAILPOST 0  // careful steps: the tail's bits and window taken after the loop
 #endif
+#ifndef DD_WMERGE
+#define DD_WMERGE 0  // item decoder (with DD_MERGE): the warm-up through the same inlined decoder
+#endif
 #ifndef DD_MERGE
 #define DD_MERGE 1  // item decoder: the item's decode and its re-decodes share one inlined copy
                     // (instances without a budget: those whose later pieces warm up)
@@ -2883,7 +2886,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
-      if (spec) {
+      constexpr bool kWMerge = DD_WMERGE && DD_MERGE && BI == 0;
+      if (spec && !kWMerge) {  // (kWMerge: the first pass of the verify loop)
         uint32_t bp = 8u * (s - DD_OV - IBX);
         DiscardSink dk;
         const DDRun rw = dd_run<DiscardSink, DD_WSYNC != 0>(S.T, inp, bp, bs, bend, dk, dctr DD_SPASS);
@@ -2923,18 +2927,36 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- verify the later items against the previous item's exit
       // (DD_MERGE: one inlined decoder for the item and its re-decodes -- a
       // pass decodes the lanes marked run_ from `start`, then verifies)
-      bool run_ = kMerge && valid && !dead;
-      uint32_t start = entry;
-      for (uint32_t iter = 0; iter <= WAVE + (kMerge ? 1u : 0u); ++iter) {
+      // (kWMerge: the warm-up is that decoder's first pass too, to the first
+      // boundary >= bs through its careful steps, its symbols written and
+      // then overwritten; a tail or EOS before bs leaves the entry unknown)
+      bool run_ = kWMerge ? spec : (kMerge && valid && !dead);
+      bool warm = kWMerge;  // (uniform) this pass is the warm-up
+      uint32_t start = kWMerge ? 8u * (s - DD_OV - IBX) : entry;
+      for (uint32_t iter = 0; iter <= WAVE + (kWMerge ? 2u : kMerge ? 1u : 0u); ++iter) {
         if (kMerge && __ballot(run_)) {
           if (run_) {
             DISink s3(my_ob);
             uint32_t bq = start;
-            rr = dd_run(S.T, inp, bq, bstop, bend, s3, dctr DD_SPASS);
-            my_exit = rr.failed ? XFAIL : bq;
-            c0 = s3.count();
+            const DDRun r2 = dd_run(S.T, inp, bq, warm ? bs : bstop, bend, s3, dctr DD_SPASS);
+            if (warm) {
+              entry = bq;
+              dead = r2.failed || bq < bs;
+            } else {
+              rr = r2;
+              my_exit = rr.failed ? XFAIL : bq;
+              c0 = s3.count();
+            }
           }
           run_ = false;
+        }
+        if (kWMerge && warm) {  // the item pass next
+          warm = false;
+          my_entry = dead ? XUNKNOWN : entry;
+          my_exit = entry;
+          start = entry;
+          run_ = valid && !dead;
+          continue;
         }
         const uint32_t up = __shfl_up(my_exit, 1, 64);
         const uint32_t pred = lane ? up : carry_exit;
