@@ -404,10 +404,15 @@ __device__ __forceinline__ uint32_t piece_bits(const PieceBytes &pb, const uint8
   return bits;
 }
 
-// Uniform maximum over the wave.
+// Uniform maximum / minimum over the wave.
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
   for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
   return __builtin_amdgcn_readfirstlane(v);
 }
 
@@ -3356,6 +3361,528 @@ __global__ __launch_bounds__(WG) void k_frame_copy(const uint8_t *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
+// Lane decoder (DESIGN.md "decode"): one lane decodes one whole string
+// (lib/nghttp2_hd_huffman.c:111-143 with fin = 1, exact entries -- no pieces,
+// no warm-up, no verify).
+//
+// A workgroup owns a contiguous window of strings and orders it by encoded
+// length in LDS (128 length classes, longest first); its waves then claim
+// groups of 64 strings of that order, one string per lane, so the lanes of
+// a wave have about the same number of bits to decode and the longest
+// strings start first.  A lane's input streams through a 64-byte ring in LDS
+// (four 16-byte chunks, dword-major so that the refill reads of the 64 lanes
+// never share a bank); chunks are loaded DL_D periods before they are
+// written to the ring, one (unconditional) load per period, so the wait for
+// a chunk is a counted vmcnt that long loads have met.  The output goes
+// through a 32-byte LDS buffer that leaves as whole 16-byte blocks.  Slots:
+// decode_batch_auto's 16-byte aligned slots (dl_slot), or the caller's
+// (decode_batch: only decoded bytes inside the slot are written).
+// ---------------------------------------------------------------------------
+#ifndef DL_WAVES
+#define DL_WAVES 16
+#endif
+#ifndef DL_LB
+#define DL_LB 13
+#endif
+#ifndef DL_D
+#define DL_D 4         // staged chunk loads in flight per lane (periods of lead)
+#endif
+#ifndef DL_STAMPS
+#define DL_STAMPS 0    // diagnostic build only: per-wave phase cycles
+#endif
+#ifndef DL_ABL
+#define DL_ABL 0       // ablation builds only (tools/diag): 1 no fast-period stores, 2 no staged loads
+#endif
+#ifndef DL_LDP
+#define DL_LDP 0       // cache policy of the staged chunk loads (A/B builds: 1 nt, 2 sc0 sc1)
+#endif
+#ifndef DL_STP
+#define DL_STP 0       // cache policy of the block stores (A/B builds: 1 nt)
+#endif
+#if DL_LDP == 1
+#define DL_LDPOL " nt"
+#elif DL_LDP == 2
+#define DL_LDPOL " sc0 sc1"
+#else
+#define DL_LDPOL ""
+#endif
+#if DL_STP == 1
+#define DL_STPOL " nt"
+#else
+#define DL_STPOL ""
+#endif
+#define DL_NT (WAVE * DL_WAVES)
+#define DL_P 3u        // pairs per period (one input / output service per period)
+#define DL_RING 16u    // input ring dwords per lane (four chunks)
+#define DL_OB 32u      // output buffer bytes per lane
+#define DL_CLASSES 128u
+#define DL_WMAX 8192u  // strings sorted at once by a workgroup
+#define DL_NONE 0xFFFFFFFFu
+#define DL_OOB 0xFFFFFFF0u  // a buffer offset past every descriptor's range
+
+struct DLShared {
+  DecT<DL_LB> T;                                        // the lookup at LDS offset 0
+  uint32_t ring[DL_WAVES][DL_RING * WAVE];              // dword j of lane l at [64 j + l]
+  alignas(16) uint32_t ob[DL_WAVES][WAVE * DL_OB / 4];  // lane l at bytes [32 l, 32 l + 32)
+  uint16_t order[DL_WMAX];                              // the window in decode order
+  uint32_t hist[DL_CLASSES];
+  uint32_t claimed;
+};
+
+#if DL_STAMPS
+__device__ unsigned long long g_dl_stamps[2048][12];
+#define DLS_INIT() unsigned long long dls[12] = {}, dlt = __builtin_amdgcn_s_memtime(), dlb = dlt
+#define DLS(slot)                                                              \
+  do {                                                                         \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime();               \
+    dls[slot] += t1_ - dlt;                                                    \
+    dlt = t1_;                                                                 \
+  } while (0)
+#define DLS_CNT(slot) (++dls[slot])
+#define DLS_FLUSH()                                                            \
+  do {                                                                         \
+    dls[11] = __builtin_amdgcn_s_memtime() - dlb;                              \
+    if (lane == 0)                                                             \
+      for (int s_ = 0; s_ < 12; ++s_) g_dl_stamps[(blockIdx.x * DL_WAVES + wv) & 2047][s_] = dls[s_]; \
+  } while (0)
+#else
+#define DLS_INIT() do { } while (0)
+#define DLS(slot) do { } while (0)
+#define DLS_CNT(slot) do { } while (0)
+#define DLS_FLUSH() do { } while (0)
+#endif
+
+// (an explicit integer minimum: HIP's min() picks a floating overload for
+// 64-bit integers)
+__device__ __host__ __forceinline__ uint64_t u64min(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// decode_batch_auto's slot of string s: 16 * (ceil(floor(8 x_s / 5) / 16) + s),
+// x_s = off[s] - off[0].  Each slot is 16-byte aligned and a multiple of 16
+// bytes, at least floor(8 E_s / 5) + 1 (the reference's allocation,
+// lib/nghttp2_hd.c:2080-2082), so whole 16-byte blocks of a string's output
+// stay inside its slot.
+__device__ __host__ __forceinline__ uint64_t dl_slot(uint32_t x, uint32_t s) {
+  const uint64_t g = ((uint64_t)x * 8u) / 5u;
+  return 16u * (((g + 15u) >> 4) + s);
+}
+
+// Length class, 0 = longest: 2-byte classes below 64 encoded bytes, 8 up to
+// 256, 32 up to 1 KiB, 128 up to 4 KiB, then powers of two.
+__device__ __forceinline__ uint32_t dl_class(uint32_t E) {
+  uint32_t c;
+  if (E < 64u) c = E >> 1;
+  else if (E < 256u) c = 32u + ((E - 64u) >> 3);
+  else if (E < 1024u) c = 56u + ((E - 256u) >> 5);
+  else if (E < 4096u) c = 80u + ((E - 1024u) >> 7);
+  else c = min(104u + (31u - (uint32_t)__builtin_clz(E)) - 12u, DL_CLASSES - 1u);
+  return DL_CLASSES - 1u - c;
+}
+
+// Chunk staging in AGPRs (this kernel has no MFMA; nothing else of the
+// compiler's lives there): slot J is a[4J .. 4J+3], written only by these
+// inline-asm loads and read only after an explicit counted wait, so no load
+// is ever in flight into a register the compiler owns (cdna_hip_programming.md
+// 5.7 item 1; nghttp2_amd/tools/check_agpr.py audits every build).  The
+// compiler does not count these loads: its own waits are not pulled down to
+// them.  The fast periods' loads and stores are exec-masked to the lanes that
+// have a chunk to take or a block to store (out-of-range lanes would still
+// take address-unit cycles), and each is issued every period -- with one lane
+// at an out-of-range offset when no lane has one, so EXEC is never 0 -- so
+// that every period issues exactly one load and one store.
+#define DL_AG_LOAD(A0, A1, A2, A3, AR)                                                   \
+  asm volatile("v_cmp_ne_u32 vcc, 0, %1\n\ts_nop 1\n\ts_and_saveexec_b64 %0, vcc\n\t"   \
+               "s_nop 4\n\tbuffer_load_dwordx4 " AR ", %2, %3, 0 offen" DL_LDPOL "\n\t"   \
+               "s_mov_b64 exec, %0"                                                      \
+               : "=&s"(saved)                                                            \
+               : "v"(pred), "v"(voff), "s"(rsrc)                                         \
+               : "vcc", A0, A1, A2, A3, "memory")
+template <int J>
+__device__ __forceinline__ void dl_stage_load(uint32_t pred, uint32_t voff, __amdgpu_buffer_rsrc_t rsrc) {
+  uint64_t saved;
+  if (J == 0) DL_AG_LOAD("a0", "a1", "a2", "a3", "a[0:3]");
+  if (J == 1) DL_AG_LOAD("a4", "a5", "a6", "a7", "a[4:7]");
+  if (J == 2) DL_AG_LOAD("a8", "a9", "a10", "a11", "a[8:11]");
+  if (J == 3) DL_AG_LOAD("a12", "a13", "a14", "a15", "a[12:15]");
+}
+#undef DL_AG_LOAD
+// a 16-byte store by the lanes with pred set (same issue rule); the trailing
+// s_nop keeps the next instruction off the data registers until the store
+// has read them
+__device__ __forceinline__ void dl_store16(uint32_t pred, uint32_t voff, u32x4 data,
+                                           __amdgpu_buffer_rsrc_t rsrc) {
+  uint64_t saved;
+  asm volatile("v_cmp_ne_u32 vcc, 0, %1\n\ts_nop 1\n\ts_and_saveexec_b64 %0, vcc\n\t"
+               "s_nop 4\n\tbuffer_store_dwordx4 %3, %2, %4, 0 offen" DL_STPOL "\n\ts_mov_b64 exec, %0\n\ts_nop 1"
+               : "=&s"(saved)
+               : "v"(pred), "v"(voff), "v"(data), "s"(rsrc)
+               : "vcc", "memory");
+}
+// The staged chunk of slot J, after its load: N younger memory instructions
+// may still be in flight (every fast period issues one load and one store, so
+// the load of DL_D periods ago has 2 DL_D - 1 younger ones).
+#define DL_AG_READ(N, A0, A1, A2, A3)                                                    \
+  asm volatile("s_waitcnt vmcnt(" #N ")\n\tv_accvgpr_read_b32 %0, " A0                   \
+               "\n\tv_accvgpr_read_b32 %1, " A1 "\n\tv_accvgpr_read_b32 %2, " A2         \
+               "\n\tv_accvgpr_read_b32 %3, " A3                                          \
+               : "=v"(v.x), "=v"(v.y), "=v"(v.z), "=v"(v.w)                              \
+               :                                                                         \
+               : "memory")
+template <int J>
+__device__ __forceinline__ u32x4 dl_stage_read() {
+  u32x4 v;
+  if (J == 0) DL_AG_READ(7, "a0", "a1", "a2", "a3");
+  if (J == 1) DL_AG_READ(7, "a4", "a5", "a6", "a7");
+  if (J == 2) DL_AG_READ(7, "a8", "a9", "a10", "a11");
+  if (J == 3) DL_AG_READ(7, "a12", "a13", "a14", "a15");
+  return v;
+}
+#undef DL_AG_READ
+__device__ __forceinline__ void dl_stage_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <bool AUTO>
+__global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restrict__ src,
+                                                        const uint32_t *__restrict__ off, uint32_t n,
+                                                        uint32_t win, uint32_t sorted,
+                                                        uint8_t *__restrict__ dst, uint64_t dst_cap,
+                                                        uint32_t *__restrict__ dst_off,
+                                                        int32_t *__restrict__ status,
+                                                        uint16_t *__restrict__ fstate_out,
+                                                        uint8_t *__restrict__ flags_out) {
+  __shared__ DLShared S;
+  constexpr uint32_t LB = DL_LB, G2 = 2u * DL_LB;  // a fast pair needs 2 LB bits of the string
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  lds_u32 *ring = (lds_u32 *)S.ring[wv] + lane;
+  lds_u8 *ob = (lds_u8 *)S.ob[wv] + lane * DL_OB;
+  stage_dec_tables(S.T, DL_NT);
+  const DecT<DL_LB> &T = S.T;
+  DLS_INIT();
+  const uint32_t off0 = __builtin_amdgcn_readfirstlane(off[0]);
+  // buffer descriptors: reads past the pool's readable end (align16(off[n]) +
+  // 16) and stores past dst_cap are dropped, so a lane with nothing to load or
+  // store in a period issues its load / store at DL_OOB
+  const uint32_t src_lim = __builtin_amdgcn_readfirstlane(
+      (uint32_t)u64min((((uint64_t)off[n] + 15u) & ~15ull) + 16u, (uint64_t)DL_OOB));
+  // (inputs made provably uniform, so the compiler keeps the descriptors in
+  // SGPRs instead of wrapping every buffer op in a waterfall loop)
+  auto uni_ptr = [](const void *p) -> void * {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (void *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  };
+  void *const src_u = uni_ptr(src);
+#define DL_RD() __builtin_amdgcn_make_buffer_rsrc(src_u, 0, (int)src_lim, 0x00020000)
+  const uint32_t dst_lim = __builtin_amdgcn_readfirstlane((uint32_t)(AUTO ? u64min(dst_cap, (uint64_t)DL_OOB) : DL_OOB));
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(dst), 0, (int)dst_lim, 0x00020000);
+  // this workgroup's window of strings, sorted DL_WMAX at a time
+  const uint32_t r0 = min(n, blockIdx.x * win), r1 = min(n, r0 + win);
+  for (uint32_t w0 = r0; w0 < r1; w0 += DL_WMAX) {
+    const uint32_t wn = min(DL_WMAX, r1 - w0), ngr = (wn + 63u) / 64u;
+    __syncthreads();  // (the previous sub-window's waves are done with order[])
+    if (sorted) {
+      for (uint32_t c = threadIdx.x; c < DL_CLASSES; c += DL_NT) S.hist[c] = 0u;
+      __syncthreads();
+      constexpr uint32_t PT = DL_WMAX / DL_NT;
+      uint32_t cls[PT];
+#pragma unroll
+      for (uint32_t u = 0; u < PT; ++u) {
+        const uint32_t t = threadIdx.x + u * DL_NT;
+        cls[u] = t < wn ? dl_class(off[w0 + t + 1] - off[w0 + t]) : 0u;
+        if (t < wn) atomicAdd((uint32_t *)&S.hist[cls[u]], 1u);
+      }
+      __syncthreads();
+      if (wv == 0) {  // exclusive scan of the 128 class counts, two per lane
+        const uint32_t h0 = S.hist[2u * lane], h1 = S.hist[2u * lane + 1u];
+        const uint32_t inc = wave_incl_scan(h0 + h1);
+        S.hist[2u * lane] = inc - h0 - h1;
+        S.hist[2u * lane + 1u] = inc - h1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < PT; ++u) {
+        const uint32_t t = threadIdx.x + u * DL_NT;
+        if (t < wn) S.order[atomicAdd((uint32_t *)&S.hist[cls[u]], 1u)] = (uint16_t)t;
+      }
+    }
+    if (threadIdx.x == 0) S.claimed = 0u;
+    __syncthreads();
+    DLS(0);
+    // Groups are claimed one ahead: the next group's string offsets are
+    // loaded when the current one starts, its first four input chunks when
+    // the current one's fast phase ends.
+    auto claim = [&]() -> uint32_t {
+      uint32_t gi = 0;
+      if (lane == 0) gi = atomicAdd((uint32_t *)&S.claimed, 1u);
+      return __builtin_amdgcn_readfirstlane(gi);
+    };
+    auto load_meta = [&](uint32_t gg) -> uint4 {  // {string, first byte, end}
+      const uint32_t q = gg * 64u + lane;
+      if (gg >= ngr || q >= wn) return make_uint4(DL_NONE, 0u, 0u, 0u);
+      const uint32_t s = w0 + (sorted ? (uint32_t)S.order[q] : q);
+      return make_uint4(s, off[s], off[s + 1], 0u);
+    };
+    auto chunk_ok = [&](const uint4 &m, uint32_t j) {  // chunk j of the string (its bytes + 7 after)
+      return m.x != DL_NONE && m.z >= m.y && m.y >= off0 && j <= ((m.z + 7u - (m.y & ~15u)) >> 4);
+    };
+    u32x4 cn[4];
+    auto load_chunks = [&](const uint4 &m) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        cn[j] = u32x4{0u, 0u, 0u, 0u};
+        if (chunk_ok(m, j)) cn[j] = __builtin_amdgcn_raw_buffer_load_b128(DL_RD(), (m.y & ~15u) + 16u * j, 0, 0);
+      }
+    };
+    uint32_t g = claim();
+    uint4 mn = load_meta(g);
+    load_chunks(mn);
+    while (g < ngr) {
+      DLS_CNT(9);
+      const uint4 mc = mn;
+      const bool have = mc.x != DL_NONE;
+      const uint32_t i = have ? mc.x : 0u, a = mc.y, b = mc.z;
+      const bool bad = have && (b < a || a < off0 || b - a >= (1u << 28));
+      const bool act = have && !bad;
+      const uint32_t E = act ? b - a : 0u;
+      // ---- input: chunks 0..3 into the ring, the bit buffer from the first byte
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        ring[64u * (4u * j)] = __builtin_bswap32(cn[j].x);
+        ring[64u * (4u * j + 1u)] = __builtin_bswap32(cn[j].y);
+        ring[64u * (4u * j + 2u)] = __builtin_bswap32(cn[j].z);
+        ring[64u * (4u * j + 3u)] = __builtin_bswap32(cn[j].w);
+      }
+      const uint32_t gn = claim();
+      mn = load_meta(gn);
+      // ---- output window [o, o + cap)
+      uint32_t o = 0, cap = 0;
+      bool slot_ovf = false;
+      if (AUTO) {
+        const uint64_t s0 = dl_slot(a - off0, i), s1 = act ? dl_slot(b - off0, i + 1u) : s0;
+        o = (uint32_t)u64min(s0, dst_cap);
+        cap = (uint32_t)(u64min(s1, dst_cap) - o);
+        slot_ovf = s1 > dst_cap;
+        if (have) {
+          dst_off[i] = o;
+          if (i == n - 1u) dst_off[n] = (uint32_t)u64min(dl_slot(off[n] - off0, n), dst_cap);
+        }
+      } else if (have) {
+        o = dst_off[i];
+        const uint32_t o1 = dst_off[i + 1];
+        cap = o1 >= o ? o1 - o : 0u;
+      }
+      const uint32_t c0 = a & ~15u;
+      const uint32_t jmax = act ? (b + 7u - c0) >> 4 : 0u;  // the last chunk the lane reads
+      const uint32_t m0 = (a & 15u) >> 2, r8 = 8u * (a & 3u);
+      // bb: the stream bits from the string's first one, MSB first, nb of them
+      // (the valid bits always end on a stream dword boundary)
+      uint64_t bb = ((((uint64_t)ring[64u * m0]) << 32) | ring[64u * (m0 + 1u)]) << r8;
+      uint32_t nb = 64u - r8, k = m0 + 2u;  // k: the next ring dword to take, prefetched in nxt
+      uint32_t nxt = ring[64u * k];
+      uint32_t rem = 8u * E;           // string bits left
+      // chunk staging: slot j (visited every DL_D-th period) holds chunk sc[j]
+      // until its visit commits it to the ring; a chunk is loaded only once
+      // its ring rows are free, so that visit always commits it
+      uint32_t cc = 4u, nl = 4u;       // chunks committed to the ring / the next one to load
+      uint32_t sc[DL_D];
+#pragma unroll
+      for (uint32_t j = 0; j < DL_D; ++j) sc[j] = DL_NONE;
+      // ---- output buffer: byte 0 <-> global offset G (16-aligned).  Whole
+      // blocks inside the window leave at once; a partial one (the head of an
+      // unaligned caller slot, or the block across the window's end) waits in
+      // registers for the string's end.
+      uint32_t G = o & ~15u;
+      lds_u8 *ptr = ob + (o & 15u);
+      const uint32_t wend = o + cap;
+      u32x4 hv = {0, 0, 0, 0}, tv = {0, 0, 0, 0};
+      uint32_t hG = DL_NONE, tG = DL_NONE;
+      auto flush = [&]() {  // exactly one store instruction per call (see dl_store16)
+        const bool fl = ptr - ob >= 16;
+        const u32x4 blk = *(const lds_u32x4 *)ob;
+        const bool full = fl && G >= o && G + 16u <= wend;
+        const bool none = !__ballot(full);
+        if (!(DL_ABL & 1)) dl_store16(full || (none && lane == 0u), full ? G : DL_OOB, blk, wr);
+        if (fl) {
+          if (!full && G < o) {
+            hv = blk;
+            hG = G;
+          } else if (!full && G < wend && tG == DL_NONE) {
+            tv = blk;
+            tG = G;
+          }
+          *(lds_u32x4 *)ob = *(const lds_u32x4 *)(ob + 16);
+          ptr -= 16;
+          G += 16u;
+        }
+      };
+#define DL_REFILL()                                                      \
+  do {                                                                   \
+    const bool t_ = nb < 32u;                                            \
+    bb |= (uint64_t)(t_ ? nxt : 0u) << ((32u - nb) & 63u);               \
+    nb += t_ ? 32u : 0u;                                                 \
+    k += t_ ? 1u : 0u;                                                   \
+    nxt = ring[64u * (k & (DL_RING - 1u))];                              \
+  } while (0)
+      bool failed = false, stopf = false;  // stopf: the string's tail met in a fast pair
+      DLS(1);
+      // ---- fast periods: a service (store, commit, load), then DL_P pairs
+      for (bool more = true; more;) {
+        static_assert(DL_D == 4, "four AGPR staging slots, vmcnt(7)");
+#pragma unroll
+        for (uint32_t j = 0; j < DL_D; ++j) {
+          const bool want = act && !failed && !stopf && rem >= G2;
+          if (!__ballot(want)) {
+            more = false;
+            break;
+          }
+          DLS_CNT(10);
+          flush();
+          if (sc[j] != DL_NONE) {  // chunk cc, loaded DL_D periods ago
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (DL_ABL & 2) {
+            } else if (j == 0) v = dl_stage_read<0>();
+            else if (j == 1) v = dl_stage_read<1>();
+            else if (j == 2) v = dl_stage_read<2>();
+            else if (j == 3) v = dl_stage_read<3>();
+            const uint32_t rr = 4u * (cc & 3u);
+            ring[64u * rr] = __builtin_bswap32(v.x);
+            ring[64u * (rr + 1u)] = __builtin_bswap32(v.y);
+            ring[64u * (rr + 2u)] = __builtin_bswap32(v.z);
+            ring[64u * (rr + 3u)] = __builtin_bswap32(v.w);
+            ++cc;
+            sc[j] = DL_NONE;
+          }
+          // one load per period (see dl_stage_load), by the lanes with a chunk
+          // to take: the next one, once chunk nl - 4 is used up
+          const bool ld = nl <= jmax && k >= 4u * (nl - 3u);
+          const uint32_t lp = (ld || (!__ballot(ld) && lane == 0u)) ? 1u : 0u;
+          const uint32_t voff = ld ? c0 + 16u * nl : DL_OOB;
+          if (DL_ABL & 2) {
+          } else if (j == 0) dl_stage_load<0>(lp, voff, DL_RD());
+          else if (j == 1) dl_stage_load<1>(lp, voff, DL_RD());
+          else if (j == 2) dl_stage_load<2>(lp, voff, DL_RD());
+          else if (j == 3) dl_stage_load<3>(lp, voff, DL_RD());
+          if (ld) sc[j] = nl++;
+          DLS(2);
+          // a lane runs its pairs when the ring holds the dwords they can
+          // take (two per pair), or when every chunk of its string is in (the
+          // ring rows past them are bits after the string end: never taken)
+          bool run = want && (4u * cc - k >= 2u * DL_P + 1u || cc > jmax);
+#pragma unroll
+          for (uint32_t p = 0; p < DL_P; ++p) {
+            if (run) {
+              const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - LB)];
+              const uint32_t U1 = E_USED(e1);
+              bb <<= U1;
+              const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - LB)];
+              const uint32_t U2 = E_USED(e2);
+              bb <<= U2;
+              ptr[0] = (uint8_t)e1;
+              ptr[1] = (uint8_t)(e1 >> 8);
+              ptr += E_CNT8(e1) >> 3;
+              ptr[0] = (uint8_t)e2;
+              ptr[1] = (uint8_t)(e2 >> 8);
+              ptr += E_CNT8(e2) >> 3;
+              nb -= U1 + U2;
+              rem -= U1 + U2;
+              DL_REFILL();
+              if (e2 == 0u) {  // a code longer than the lookup (an e1 of 0 stalls e2 too)
+                const uint32_t e_ = slow_entry(T, (uint32_t)(bb >> 32), rem);
+                if (e_ == 0xFFFFFFFFu) {
+                  failed = true;  // EOS: the FSM's sticky failure state
+                } else if (E_L1(e_) > rem) {
+                  stopf = true;   // the string's tail: the careful steps take it
+                } else {
+                  ptr[0] = (uint8_t)e_;
+                  ptr += 1;
+                  const uint32_t U_ = E_USED(e_);
+                  bb <<= U_;
+                  nb -= U_;
+                  rem -= U_;
+                  DL_REFILL();
+                }
+              }
+              run = !failed && !stopf && rem >= G2;
+            }
+          }
+          DLS(3);
+        }
+      }
+#undef DL_REFILL
+      dl_stage_drain();  // (no staged load in flight past the fast periods)
+      load_chunks(mn);  // the next group's first chunks, in flight over this one's tail
+      flush();
+      // ---- careful steps: the last < 2 LB bits (or a long code at the tail),
+      // each step predicated on the string end instead of branching
+      uint32_t t_bits = 0, t_win = 0;
+      bool done = !act || failed;
+      while (__ballot(!done)) {
+        const uint32_t w = (uint32_t)(bb >> 32);
+        const bool stop = done || rem == 0u;
+        uint32_t e = T.lut[w >> (32 - LB)];
+        const bool slow = e == 0u && !stop;
+        if (__ballot(slow)) {
+          if (slow) e = slow_entry(T, w, rem);
+        }
+        const bool eos = e == 0xFFFFFFFFu && !stop;
+        const uint32_t L1 = E_L1(e), U = E_USED(e);
+        const bool take1 = !stop && !eos && L1 <= rem;
+        const bool take2 = take1 && E_CNT(e) == 2u && U <= rem;
+        const bool tail = !stop && !eos && !take1;  // a proper prefix of a code
+        t_bits = tail ? rem : t_bits;
+        t_win = tail ? w : t_win;
+        const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
+        if (take1) {
+          ptr[0] = (uint8_t)e;
+          ptr[1] = (uint8_t)(e >> 8);
+          ptr += take2 ? 2 : 1;
+        }
+        bb <<= adv;
+        rem -= adv;
+        failed = failed || eos;
+        done = done || eos || !take1 || rem == 0u;
+      }
+      DLS(4);
+      // ---- the rest of the output, status and final decode context
+      flush();
+      const uint32_t nsym = G + (uint32_t)(ptr - ob) - o;
+      if (act) {
+        // AUTO: the last block may hold bytes past the string (inside its slot)
+        const uint32_t hi = AUTO ? wend : o + min(cap, nsym);
+        auto put_bytes = [&](const u32x4 &v, uint32_t Gb) {
+          for (uint32_t x = 0; x < 16u; ++x) {
+            const uint32_t q = Gb + x;
+            if (q >= o && q < hi) dst[q] = (uint8_t)(v[x >> 2] >> (8u * (x & 3u)));
+          }
+        };
+        if (hG != DL_NONE) put_bytes(hv, hG);
+        if (tG != DL_NONE) put_bytes(tv, tG);
+        if (ptr > ob) {
+          const u32x4 v = *(const lds_u32x4 *)ob;
+          if (G >= o && G + 16u <= hi) *reinterpret_cast<uint4 *>(dst + G) = make_uint4(v.x, v.y, v.z, v.w);
+          else put_bytes(v, G);
+        }
+      }
+      if (have) {
+        if (bad) {
+          status[i] = NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+          if (fstate_out) {
+            fstate_out[i] = 0u;
+            flags_out[i] = 0u;
+          }
+        } else {
+          dd_finish(T, failed, t_bits, t_win, nsym, AUTO ? slot_ovf : nsym > cap, i, status,
+                    fstate_out, flags_out);
+        }
+      }
+      g = gn;
+      DLS(5);
+    }
+  }
+  DLS_FLUSH();
+#undef DL_RD
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 static inline uint32_t ntiles_for(uint32_t n) { return (n + WG - 1) / WG; }
@@ -3466,7 +3993,51 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   return hip_rv(hipGetLastError());
 }
 
+// The lane decoder: AUTO slots (written to dst_off) or the caller's slots.
+// Each resident workgroup takes a window of ceil(n / grid) strings (whole
+// groups of 64) and, when `sort`, decodes it in length order.
+template <bool AUTO>
+static int decode_lanes(const uint8_t *src, const uint32_t *src_off, uint32_t n, uint8_t *dst,
+                        size_t dst_cap, uint32_t *dst_off, int32_t *status, uint16_t *fstate,
+                        uint8_t *flags, void *stream, bool sort) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AUTO ? hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st)) : 0;
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (AUTO && (uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  const uint32_t grid = persistent_grid<k_decode_lanes<AUTO>, DL_NT, 64>(n);
+  const uint32_t win = (uint32_t)((((uint64_t)n + grid - 1u) / grid + 63u) & ~63ull);
+  hipLaunchKernelGGL((k_decode_lanes<AUTO>), dim3(grid), dim3(DL_NT), 0, st, src, src_off, n, win,
+                     sort ? 1u : 0u, dst, (uint64_t)dst_cap, dst_off, status, fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
 extern "C" {
+
+// Lane decoder, A/B entry: mode bit 0 = the caller's slots (decode_batch
+// semantics; dst_cap ignored), bit 1 = string order (no length sort).
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__decode_batch_lanes(const uint8_t *src, const uint32_t *src_off,
+                                                          uint32_t n, uint8_t *dst, size_t dst_cap,
+                                                          uint32_t *dst_off, int32_t *status,
+                                                          uint16_t *fstate, uint8_t *flags,
+                                                          void *stream, int mode) {
+  const bool sort = !(mode & 2);
+  if (mode & 1)
+    return decode_lanes<false>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags,
+                               stream, sort);
+  return decode_lanes<true>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, stream,
+                            sort);
+}
+#if DL_STAMPS
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__dl_stamps(void *out, int reset) {
+  if (reset) {
+    static unsigned long long z[2048][12];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dl_stamps), z, sizeof(z));
+  }
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dl_stamps), sizeof(unsigned long long) * 2048 * 12);
+}
+#endif
 
 const char *nghttp2_amd_hd_version(void) { return "nghttp2_amd_hd 0.2.0 gfx950"; }
 
