@@ -3423,7 +3423,7 @@ __global__ __launch_bounds__(WG) void k_frame_copy(const uint8_t *__restrict__ s
 struct DLShared {
   DecT<DL_LB> T;                                        // the lookup at LDS offset 0
   uint32_t ring[DL_WAVES][DL_RING * WAVE];              // dword j of lane l at [64 j + l]
-  alignas(16) uint32_t ob[DL_WAVES][WAVE * DL_OB / 4];  // lane l at bytes [32 l, 32 l + 32)
+  uint32_t ob[DL_WAVES][DL_OB / 4 * WAVE];             // output dword j of lane l at [64 j + l]
   uint16_t order[DL_WMAX];                              // the window in decode order
   uint32_t hist[DL_CLASSES];
   uint32_t claimed;
@@ -3552,7 +3552,7 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
   constexpr uint32_t LB = DL_LB, G2 = 2u * DL_LB;  // a fast pair needs 2 LB bits of the string
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   lds_u32 *ring = (lds_u32 *)S.ring[wv] + lane;
-  lds_u8 *ob = (lds_u8 *)S.ob[wv] + lane * DL_OB;
+  lds_u32 *ob = (lds_u32 *)S.ob[wv] + lane;
   stage_dec_tables(S.T, DL_NT);
   const DecT<DL_LB> &T = S.T;
   DLS_INIT();
@@ -3686,18 +3686,27 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
       uint32_t sc[DL_D];
 #pragma unroll
       for (uint32_t j = 0; j < DL_D; ++j) sc[j] = DL_NONE;
-      // ---- output buffer: byte 0 <-> global offset G (16-aligned).  Whole
-      // blocks inside the window leave at once; a partial one (the head of an
-      // unaligned caller slot, or the block across the window's end) waits in
-      // registers for the string's end.
-      uint32_t G = o & ~15u;
-      lds_u8 *ptr = ob + (o & 15u);
+      // ---- output: the decoded bytes gather in a 64-bit register (acc, nacc
+      // bits, little-endian) and leave it as whole dwords into the lane's
+      // 8-dword LDS ring (dword q of the output from G0 = o & ~15 at row q & 7;
+      // wq dwords complete, the partial one is rewritten in place at row wq).
+      // Whole 16-byte blocks inside the window leave at once; a partial one
+      // (the head of an unaligned caller slot, or the block across the
+      // window's end) waits in registers for the string's end.
+      const uint32_t G0 = o & ~15u;
+      uint32_t G = G0, wq = (o & 15u) >> 2, fq = 0;  // fq: dwords flushed
+      uint64_t acc = 0;
+      uint32_t nacc = 8u * (o & 3u);
       const uint32_t wend = o + cap;
       u32x4 hv = {0, 0, 0, 0}, tv = {0, 0, 0, 0};
       uint32_t hG = DL_NONE, tG = DL_NONE;
+      auto rdblk = [&]() {
+        return u32x4{ob[64u * (fq & 7u)], ob[64u * ((fq + 1u) & 7u)], ob[64u * ((fq + 2u) & 7u)],
+                     ob[64u * ((fq + 3u) & 7u)]};
+      };
       auto flush = [&]() {  // exactly one store instruction per call (see dl_store16)
-        const bool fl = ptr - ob >= 16;
-        const u32x4 blk = *(const lds_u32x4 *)ob;
+        const bool fl = wq - fq >= 4u;
+        const u32x4 blk = rdblk();
         const bool full = fl && G >= o && G + 16u <= wend;
         const bool none = !__ballot(full);
         if (!(DL_ABL & 1)) dl_store16(full || (none && lane == 0u), full ? G : DL_OOB, blk, wr);
@@ -3709,11 +3718,21 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
             tv = blk;
             tG = G;
           }
-          *(lds_u32x4 *)ob = *(const lds_u32x4 *)(ob + 16);
-          ptr -= 16;
+          fq += 4u;
           G += 16u;
         }
       };
+// v: up to 4 output bytes (little-endian), bits = 8 x their count
+#define DL_PUT(v, bits)                                                  \
+  do {                                                                   \
+    acc |= (uint64_t)(v) << nacc;                                        \
+    nacc += (bits);                                                      \
+    const bool em_ = nacc >= 32u;                                        \
+    ob[64u * (wq & 7u)] = (uint32_t)acc;                                 \
+    acc = em_ ? acc >> 32 : acc;                                         \
+    nacc -= em_ ? 32u : 0u;                                              \
+    wq += em_ ? 1u : 0u;                                                 \
+  } while (0)
 #define DL_REFILL()                                                      \
   do {                                                                   \
     const bool t_ = nb < 32u;                                            \
@@ -3776,12 +3795,7 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
               const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - LB)];
               const uint32_t U2 = E_USED(e2);
               bb <<= U2;
-              ptr[0] = (uint8_t)e1;
-              ptr[1] = (uint8_t)(e1 >> 8);
-              ptr += E_CNT8(e1) >> 3;
-              ptr[0] = (uint8_t)e2;
-              ptr[1] = (uint8_t)(e2 >> 8);
-              ptr += E_CNT8(e2) >> 3;
+              DL_PUT((e1 & 0xFFFFu) | ((e2 & 0xFFFFu) << E_CNT8(e1)), E_CNT8(e1) + E_CNT8(e2));
               nb -= U1 + U2;
               rem -= U1 + U2;
               DL_REFILL();
@@ -3792,8 +3806,7 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
                 } else if (E_L1(e_) > rem) {
                   stopf = true;   // the string's tail: the careful steps take it
                 } else {
-                  ptr[0] = (uint8_t)e_;
-                  ptr += 1;
+                  DL_PUT(e_ & 0xFFu, 8u);
                   const uint32_t U_ = E_USED(e_);
                   bb <<= U_;
                   nb -= U_;
@@ -3831,20 +3844,18 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
         t_bits = tail ? rem : t_bits;
         t_win = tail ? w : t_win;
         const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
-        if (take1) {
-          ptr[0] = (uint8_t)e;
-          ptr[1] = (uint8_t)(e >> 8);
-          ptr += take2 ? 2 : 1;
-        }
+        if (take1) DL_PUT(e & (take2 ? 0xFFFFu : 0xFFu), take2 ? 16u : 8u);
         bb <<= adv;
         rem -= adv;
         failed = failed || eos;
         done = done || eos || !take1 || rem == 0u;
       }
       DLS(4);
+      ob[64u * (wq & 7u)] = (uint32_t)acc;  // the partial last dword
       // ---- the rest of the output, status and final decode context
       flush();
-      const uint32_t nsym = G + (uint32_t)(ptr - ob) - o;
+#undef DL_PUT
+      const uint32_t nsym = G0 + 4u * wq + (nacc >> 3) - o;
       if (act) {
         // AUTO: the last block may hold bytes past the string (inside its slot)
         const uint32_t hi = AUTO ? wend : o + min(cap, nsym);
@@ -3856,8 +3867,8 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
         };
         if (hG != DL_NONE) put_bytes(hv, hG);
         if (tG != DL_NONE) put_bytes(tv, tG);
-        if (ptr > ob) {
-          const u32x4 v = *(const lds_u32x4 *)ob;
+        if (4u * wq + (nacc >> 3) > 4u * fq) {
+          const u32x4 v = rdblk();
           if (G >= o && G + 16u <= hi) *reinterpret_cast<uint4 *>(dst + G) = make_uint4(v.x, v.y, v.z, v.w);
           else put_bytes(v, G);
         }
@@ -3880,6 +3891,474 @@ __global__ __launch_bounds__(DL_NT) void k_decode_lanes(const uint8_t *__restric
   }
   DLS_FLUSH();
 #undef DL_RD
+}
+
+// ---------------------------------------------------------------------------
+// Lane decoder with cooperative transfers (DESIGN.md "decode"): one lane
+// decodes one whole string, as k_decode_lanes, but no lane loads or stores
+// its own bytes.  Global memory is touched only in whole 64-byte granules,
+// 16 of them per instruction (lane 4q + c moves piece c of the q-th granule):
+// a per-lane 16-byte access stream to a long string leaves partial lines in
+// L2 that are evicted long before the lane's next piece arrives, so every
+// piece cost a separate line fetch or a partial-line write.  Each period a
+// wave ranks the lanes that wait for an input block (the next 64-byte
+// aligned block of their string, once its ring rows are free) and the lanes
+// holding a complete output block, pushes each one's {address | lane} to its
+// loader quad (ds_permute + a quad broadcast), and issues at most L2_NI
+// transfers each way.  Loaded blocks are committed to the owners' input rings
+// in the next period; output blocks are read from the owners' rings, zeroed,
+// and stored at once.
+//
+// Output slots are 64-byte aligned (dl2_slot), so a string's last block is
+// stored whole (the bytes past the string inside its slot are zero): every
+// store is a full granule.  Output bits are OR-ed into the lane's ring at
+// the output bit position (ds_or, no read-modify-write in registers).
+// ---------------------------------------------------------------------------
+#ifndef L2_WAVES
+#define L2_WAVES 10
+#endif
+#define L2_NT (WAVE * L2_WAVES)
+#define L2_P 3u        // pairs per period
+// Input ring: a 64-byte block plus L2_IN - 16 dwords of margin; block j is
+// requested once dword 16 j - (L2_IN - 16) is taken, so a lane that runs a
+// period (which needs 2 L2_P dwords at most) rarely waits for one.
+#define L2_IN 24u
+// Output ring: a period adds at most 5 L2_P bytes, so with every complete
+// block stored at the start of the next period, 16 + ceil(5 L2_P / 4) + 1
+// rows (the OR touches the row after the current one) never wrap onto an
+// unstored dword.
+#define L2_OUT 21u
+#define L2_WMAX 4096u  // strings sorted at once by a workgroup
+#define L2_NI 4        // transfers per period and direction, at most
+#ifndef L2_PRIO
+#define L2_PRIO 0      // A/B: wave issue priority by the group's longest string
+#endif
+#ifndef L2_TH
+#define L2_TH 1u       // a period issues transfers once this many blocks wait (or one is urgent)
+#endif
+
+struct L2Shared {
+  DecT<13> T;                             // the lookup at LDS offset 0
+  uint32_t in[L2_WAVES][L2_IN * WAVE];    // input dword q (byte-swapped) of lane l at [64 (q mod L2_IN) + l]
+  uint32_t out[L2_WAVES][L2_OUT * WAVE];  // output dword q at [64 (q mod L2_OUT) + l]
+  uint16_t order[L2_WMAX];
+  uint32_t hist[DL_CLASSES];
+  uint32_t claimed;
+};
+static_assert(sizeof(L2Shared) <= 160u * 1024u, "lane decoder LDS");
+
+// decode_batch_auto's slot of string s: 64 * (ceil(floor(8 x_s / 5) / 64) + s),
+// x_s = off[s] - off[0]: 64-byte aligned, a multiple of 64 bytes, at least
+// floor(8 E_s / 5) + 1 (lib/nghttp2_hd.c:2080-2082).
+__device__ __host__ __forceinline__ uint64_t dl2_slot(uint32_t x, uint32_t s) {
+  const uint64_t g = ((uint64_t)x * 8u) / 5u;
+  return 64u * (((g + 63u) >> 6) + s);
+}
+
+__global__ __launch_bounds__(L2_NT) void k_decode_lanes2(const uint8_t *__restrict__ src,
+                                                         const uint32_t *__restrict__ off, uint32_t n,
+                                                         uint8_t *__restrict__ dst,
+                                                         uint64_t dst_cap, uint32_t *__restrict__ dst_off,
+                                                         int32_t *__restrict__ status,
+                                                         uint16_t *__restrict__ fstate_out,
+                                                         uint8_t *__restrict__ flags_out) {
+  __shared__ L2Shared S;
+  constexpr uint32_t LB = 13, G2 = 2u * 13u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t q4 = lane >> 2, c4 = lane & 3u;  // as a loader: granule q4 of a transfer, piece c4
+  lds_u32 *const inw = (lds_u32 *)S.in[wv];
+  lds_u32 *const outw = (lds_u32 *)S.out[wv];
+  lds_u32 *const inr = inw + lane;
+  lds_u32 *const outr = outw + lane;
+  const uint32_t off0 = __builtin_amdgcn_readfirstlane(off[0]);
+  // this workgroup's strings: a contiguous range, balanced over the grid by
+  // weight (encoded bytes + 32 per string; a 64-ary search over the offsets)
+  uint32_t r0, r1;
+  {
+    const uint32_t nwg = gridDim.x, gw = blockIdx.x;
+    const uint64_t wtot = (uint64_t)(off[n] - off0) + 32ull * n;
+    auto first_at = [&](uint64_t target) -> uint32_t {  // smallest s with weight(s) >= target
+      if (target == 0) return 0u;
+      uint32_t lo = 0, hi = n;  // weight(lo) < target <= weight(hi)
+      while (hi - lo > 1u) {
+        const uint32_t step = (hi - lo + WAVE - 1u) / WAVE;
+        const uint32_t c = min(lo + (lane + 1u) * step, hi);
+        const uint64_t wc = (uint64_t)(off[c] - off0) + 32ull * c;
+        const uint64_t ge = __ballot(wc >= target);  // (lane 63 or the clamp reaches hi)
+        const uint32_t j = ge ? (uint32_t)__builtin_ctzll(ge) : WAVE - 1u;
+        const uint32_t nhi = __builtin_amdgcn_readlane(c, j);
+        lo = j ? __builtin_amdgcn_readlane(c, j - 1u) : lo;
+        hi = nhi;
+      }
+      return hi;
+    };
+    r0 = first_at(wtot * gw / nwg);
+    r1 = gw + 1u == nwg ? n : first_at(wtot * (gw + 1u) / nwg);
+  }
+  for (uint32_t r = 0; r < L2_OUT; ++r) outr[64u * r] = 0u;
+  stage_dec_tables(S.T, L2_NT);
+  const DecT<13> &T = S.T;
+  DLS_INIT();
+  const uint32_t src_lim = __builtin_amdgcn_readfirstlane(
+      (uint32_t)u64min((((uint64_t)off[n] + 15u) & ~15ull) + 16u, (uint64_t)DL_OOB));
+  auto uni_ptr = [](const void *p) -> void * {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (void *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  };
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(src), 0, (int)src_lim, 0x00020000);
+  const uint32_t dst_lim = __builtin_amdgcn_readfirstlane((uint32_t)u64min(dst_cap, (uint64_t)DL_OOB));
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(uni_ptr(dst), 0, (int)dst_lim, 0x00020000);
+  for (uint32_t w0 = r0; w0 < r1; w0 += L2_WMAX) {
+    const uint32_t wn = min(L2_WMAX, r1 - w0), ngr = (wn + 63u) / 64u;
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < DL_CLASSES; c += L2_NT) S.hist[c] = 0u;
+    __syncthreads();
+    constexpr uint32_t PT = (L2_WMAX + L2_NT - 1u) / L2_NT;
+    uint32_t cls[PT];
+#pragma unroll
+    for (uint32_t u = 0; u < PT; ++u) {
+      const uint32_t t = threadIdx.x + u * L2_NT;
+      cls[u] = t < wn ? dl_class(off[w0 + t + 1] - off[w0 + t]) : 0u;
+      if (t < wn) atomicAdd((uint32_t *)&S.hist[cls[u]], 1u);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const uint32_t h0 = S.hist[2u * lane], h1 = S.hist[2u * lane + 1u];
+      const uint32_t inc = wave_incl_scan(h0 + h1);
+      S.hist[2u * lane] = inc - h0 - h1;
+      S.hist[2u * lane + 1u] = inc - h1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < PT; ++u) {
+      const uint32_t t = threadIdx.x + u * L2_NT;
+      if (t < wn) S.order[atomicAdd((uint32_t *)&S.hist[cls[u]], 1u)] = (uint16_t)t;
+    }
+    if (threadIdx.x == 0) S.claimed = 0u;
+    __syncthreads();
+    auto claim = [&]() -> uint32_t {
+      uint32_t gi = 0;
+      if (lane == 0) gi = atomicAdd((uint32_t *)&S.claimed, 1u);
+      return __builtin_amdgcn_readfirstlane(gi);
+    };
+    auto load_meta = [&](uint32_t gg) -> uint4 {  // {string, first byte, end}
+      const uint32_t q = gg * 64u + lane;
+      if (gg >= ngr || q >= wn) return make_uint4(DL_NONE, 0u, 0u, 0u);
+      const uint32_t s = w0 + (uint32_t)S.order[q];
+      return make_uint4(s, off[s], off[s + 1], 0u);
+    };
+    // A group's first input block and the first L2_IN - 16 dwords of the
+    // next, prefetched during the previous group's tail: transfer h < 4
+    // carries block b0 of owners 16 h .. 16 h + 15 (a quad per owner),
+    // transfer 4 + t the first 32 bytes of block b0 + 1 of owners
+    // 32 t .. 32 t + 31 (a lane pair per owner).
+    static_assert(L2_IN == 24u, "prefetch: a block and 32 bytes");
+    u32x4 pf[6];
+    auto meta_span = [&](const uint4 &m, uint32_t &av, uint32_t &bv) {
+      const bool ok = m.x != DL_NONE && m.z > m.y && m.y >= off0 && m.z - m.y < (1u << 28);
+      av = ok ? m.y : 0u;
+      bv = ok ? m.z : 0u;
+    };
+    auto prefetch = [&](const uint4 &m) {
+      uint32_t av, bv;
+      meta_span(m, av, bv);
+#pragma unroll
+      for (uint32_t h = 0; h < 4; ++h) {
+        const uint32_t oa = __shfl(av, 16 * h + q4, 64), ob = __shfl(bv, 16 * h + q4, 64);
+        const uint32_t at = ob > oa ? (oa & ~63u) + 16u * c4 : DL_OOB;
+        pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rd, at, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < 2; ++t) {
+        const uint32_t ow = 32u * t + (lane >> 1);
+        const uint32_t oa = __shfl(av, ow, 64), ob = __shfl(bv, ow, 64);
+        const uint32_t nb1 = (oa & ~63u) + 64u;
+        const uint32_t at = ob > nb1 ? nb1 + 16u * (lane & 1u) : DL_OOB;
+        pf[4 + t] = __builtin_amdgcn_raw_buffer_load_b128(rd, at, 0, 0);
+      }
+    };
+    auto commit_pf = [&](const uint4 &m) {
+      uint32_t av, bv;
+      meta_span(m, av, bv);
+      auto put4 = [&](uint32_t q, uint32_t ow, const u32x4 &v) {  // dwords q .. q + 3 of owner ow
+        uint32_t r = q % L2_IN;
+        inw[64u * r + ow] = __builtin_bswap32(v.x);
+        r = r == L2_IN - 1u ? 0u : r + 1u;
+        inw[64u * r + ow] = __builtin_bswap32(v.y);
+        r = r == L2_IN - 1u ? 0u : r + 1u;
+        inw[64u * r + ow] = __builtin_bswap32(v.z);
+        r = r == L2_IN - 1u ? 0u : r + 1u;
+        inw[64u * r + ow] = __builtin_bswap32(v.w);
+      };
+#pragma unroll
+      for (uint32_t h = 0; h < 4; ++h) {
+        const uint32_t ow = 16 * h + q4, oa = __shfl(av, ow, 64);
+        put4(((oa & ~63u) >> 2) + 4u * c4, ow, pf[h]);
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < 2; ++t) {
+        const uint32_t ow = 32u * t + (lane >> 1), oa = __shfl(av, ow, 64);
+        put4(((oa & ~63u) >> 2) + 16u + 4u * (lane & 1u), ow, pf[4 + t]);
+      }
+    };
+    uint32_t g = claim();
+    uint4 mn = load_meta(g);
+    prefetch(mn);
+    DLS(0);
+    while (g < ngr) {
+      DLS_CNT(9);
+      const uint4 mc = mn;
+      commit_pf(mc);
+      const bool have = mc.x != DL_NONE;
+      const uint32_t i = have ? mc.x : 0u, a = mc.y, b = mc.z;
+      const bool bad = have && (b < a || a < off0 || b - a >= (1u << 28));
+      const bool act = have && !bad;
+      const uint32_t E = act ? b - a : 0u;
+#if L2_PRIO
+      {  // groups of long strings set the kernel's tail: issue priority by length
+        const uint32_t em = __builtin_amdgcn_readfirstlane(wave_max(E));
+        if (em >= 512u) __builtin_amdgcn_s_setprio(3);
+        else if (em >= 256u) __builtin_amdgcn_s_setprio(2);
+        else if (em >= 128u) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#endif
+      const uint32_t gn = claim();
+      mn = load_meta(gn);
+      // ---- output slot [o, o + cap), 64-byte aligned
+      const uint64_t s0 = dl2_slot(a - off0, i), s1 = act ? dl2_slot(b - off0, i + 1u) : s0;
+      const uint32_t o = (uint32_t)u64min(s0, dst_cap);
+      const bool slot_ovf = s1 > dst_cap;
+      if (have) {
+        dst_off[i] = o;
+        if (i == n - 1u) dst_off[n] = (uint32_t)u64min(dl2_slot(off[n] - off0, n), dst_cap);
+      }
+      // ---- input: the ring holds dwords below in_end (16 b0 + L2_IN at
+      // first); nreq = the next whole block to load, requested once the
+      // dwords its rows held are taken (k >= 16 nreq - (L2_IN - 16))
+      const uint32_t lastb = act && E ? (b - 1u) >> 6 : 0u;
+      uint32_t nreq = (a >> 6) + 1u, in_end = 16u * (a >> 6) + L2_IN;
+      bool reqd = false;  // block nreq in flight (committed next period)
+      const uint32_t k0 = a >> 2, r8 = 8u * (a & 3u);
+      const uint32_t kr0 = k0 % L2_IN, kr1 = kr0 == L2_IN - 1u ? 0u : kr0 + 1u;
+      uint64_t bb = ((((uint64_t)inr[64u * kr0]) << 32) | inr[64u * kr1]) << r8;
+      uint32_t nb = 64u - r8, k = k0 + 2u, kr = kr1 == L2_IN - 1u ? 0u : kr1 + 1u;  // kr: k's row
+      uint32_t nxt = inr[64u * kr];
+      uint32_t rem = 8u * E;
+      // ---- output: P bits decoded; dword P >> 5 at ring row orow; st blocks stored
+      uint32_t P = 0, st = 0, orow = (o >> 2) % L2_OUT;
+#define L2_PUT(v, bits)                                                      \
+  do {                                                                       \
+    const uint64_t t_ = (uint64_t)(v) << (P & 31u);                          \
+    const uint32_t r1_ = orow == L2_OUT - 1u ? 0u : orow + 1u;               \
+    atomicOr((uint32_t *)&outr[64u * orow], (uint32_t)t_);                   \
+    atomicOr((uint32_t *)&outr[64u * r1_], (uint32_t)(t_ >> 32));            \
+    orow = ((P & 31u) + (bits)) >= 32u ? r1_ : orow;                         \
+    P += (bits);                                                             \
+  } while (0)
+#define L2_REFILL()                                                      \
+  do {                                                                   \
+    const bool t_ = nb < 32u;                                            \
+    bb |= (uint64_t)(t_ ? nxt : 0u) << ((32u - nb) & 63u);               \
+    nb += t_ ? 32u : 0u;                                                 \
+    k += t_ ? 1u : 0u;                                                   \
+    kr = t_ ? (kr == L2_IN - 1u ? 0u : kr + 1u) : kr;                    \
+    nxt = inr[64u * kr];                                                 \
+  } while (0)
+      // ---- transfers: rank the waiting lanes, one granule per loader quad
+      auto rank_push = [&](bool need, uint32_t payload, uint32_t &cnt, uint32_t &rank) {
+        const uint64_t m = __ballot(need);
+        cnt = (uint32_t)__popcll(m);
+        rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        (void)payload;
+      };
+      auto quad_get = [&](bool need, uint32_t rank, uint32_t ii, uint32_t payload) -> uint32_t {
+        const bool push = need && rank >= 16u * ii && rank < 16u * ii + 16u;
+        const uint32_t dl = push ? 4u * (rank - 16u * ii) : (lane | 1u);
+        const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute((int)(4u * dl), (int)payload);
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)got, 0x00, 0xf, 0xf, true);  // quad_perm [0,0,0,0]
+      };
+      auto store_service = [&](bool need, bool urgent) {
+        uint32_t cnt, rank;
+        const uint32_t payload = (o + 64u * st) | lane;
+        rank_push(need, payload, cnt, rank);
+        if (cnt == 0u || (cnt < L2_TH && !__ballot(urgent))) return;
+        const uint32_t ni = min((cnt + 15u) >> 4, (uint32_t)L2_NI);
+#pragma unroll
+        for (uint32_t ii = 0; ii < (uint32_t)L2_NI; ++ii) {
+          if (ii < ni) {
+            const uint32_t got = quad_get(need, rank, ii, payload);
+            const bool valid = q4 + 16u * ii < cnt;
+            const uint32_t ow = got & 63u, at = (got & ~63u) + 16u * c4;
+            uint32_t rr = ((at >> 2)) % L2_OUT;
+            u32x4 v;
+            v.x = outw[64u * rr + ow];
+            const uint32_t rr1 = rr == L2_OUT - 1u ? 0u : rr + 1u;
+            v.y = outw[64u * rr1 + ow];
+            const uint32_t rr2 = rr1 == L2_OUT - 1u ? 0u : rr1 + 1u;
+            v.z = outw[64u * rr2 + ow];
+            const uint32_t rr3 = rr2 == L2_OUT - 1u ? 0u : rr2 + 1u;
+            v.w = outw[64u * rr3 + ow];
+            if (valid) {
+              outw[64u * rr + ow] = 0u;
+              outw[64u * rr1 + ow] = 0u;
+              outw[64u * rr2 + ow] = 0u;
+              outw[64u * rr3 + ow] = 0u;
+            }
+            const uint32_t sa = valid && (uint64_t)at + 16u <= dst_cap ? at : DL_OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(v, wr, sa, 0, 0);
+          }
+        }
+        if (need && rank < 16u * ni) ++st;
+      };
+      u32x4 stg[L2_NI];
+      uint32_t sti[L2_NI];
+      uint32_t nld = 0;
+      auto load_service = [&](bool need, bool urgent) {
+        uint32_t cnt, rank;
+        const uint32_t payload = 64u * nreq | lane;
+        rank_push(need, payload, cnt, rank);
+        nld = 0;
+        if (cnt == 0u || (cnt < L2_TH && !__ballot(urgent))) return;
+        const uint32_t ni = min((cnt + 15u) >> 4, (uint32_t)L2_NI);
+        nld = ni;
+#pragma unroll
+        for (uint32_t ii = 0; ii < (uint32_t)L2_NI; ++ii) {
+          if (ii < ni) {
+            const uint32_t got = quad_get(need, rank, ii, payload);
+            const bool valid = q4 + 16u * ii < cnt;
+            sti[ii] = valid ? got : DL_NONE;
+            stg[ii] = __builtin_amdgcn_raw_buffer_load_b128(rd, valid ? (got & ~63u) + 16u * c4 : DL_OOB, 0, 0);
+          }
+        }
+        if (need && rank < 16u * ni) reqd = true;
+      };
+      auto commit = [&]() {
+#pragma unroll
+        for (uint32_t ii = 0; ii < (uint32_t)L2_NI; ++ii) {
+          if (ii < nld && sti[ii] != DL_NONE) {
+            uint32_t r = ((sti[ii] & ~63u) >> 2) % L2_IN + 4u * c4;
+            r = r >= L2_IN ? r - L2_IN : r;
+            const uint32_t ow = sti[ii] & 63u;
+            const u32x4 v = stg[ii];
+            inw[64u * r + ow] = __builtin_bswap32(v.x);
+            r = r == L2_IN - 1u ? 0u : r + 1u;
+            inw[64u * r + ow] = __builtin_bswap32(v.y);
+            r = r == L2_IN - 1u ? 0u : r + 1u;
+            inw[64u * r + ow] = __builtin_bswap32(v.z);
+            r = r == L2_IN - 1u ? 0u : r + 1u;
+            inw[64u * r + ow] = __builtin_bswap32(v.w);
+          }
+        }
+        nld = 0;
+        if (reqd) {
+          in_end = 16u * nreq + 16u;
+          ++nreq;
+          reqd = false;
+        }
+        nxt = inr[64u * kr];
+      };
+      bool failed = false, stopf = false;
+      DLS(1);
+      // ---- fast periods
+      for (;;) {
+        commit();
+        const bool want = act && !failed && !stopf && rem >= G2;
+        if (!__ballot(want)) break;
+        DLS_CNT(10);
+        store_service(act && (P >> 9) > st, true);  // every complete block (see L2_OUT)
+        const bool all_in = nreq > lastb;
+        const uint32_t avail = in_end - k;
+        load_service(act && !all_in && k + (L2_IN - 16u) >= 16u * nreq, false);
+        bool run = want && (all_in || avail >= 2u * L2_P) && (P >> 5) - 16u * st <= 15u;
+        DLS(2);
+#pragma unroll
+        for (uint32_t p = 0; p < L2_P; ++p) {
+          const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - LB)];
+          const uint32_t U1 = run ? E_USED(e1) : 0u;
+          bb <<= U1;
+          const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - LB)];
+          const uint32_t U2 = run ? E_USED(e2) : 0u;
+          bb <<= U2;
+          const uint32_t c1 = E_CNT8(e1);
+          const uint32_t v = run ? ((e1 & 0xFFFFu) | ((e2 & 0xFFFFu) << c1)) : 0u;
+          const uint32_t bits = run ? c1 + E_CNT8(e2) : 0u;
+          L2_PUT(v, bits);
+          nb -= U1 + U2;
+          rem -= U1 + U2;
+          L2_REFILL();
+          const bool slow = run && e2 == 0u;  // a code longer than the lookup (an e1 of 0 stalls e2 too)
+          if (__ballot(slow)) {
+            if (slow) {
+              const uint32_t e_ = slow_entry(T, (uint32_t)(bb >> 32), rem);
+              if (e_ == 0xFFFFFFFFu) {
+                failed = true;  // EOS: the FSM's sticky failure state
+              } else if (E_L1(e_) > rem) {
+                stopf = true;   // the string's tail: the careful steps take it
+              } else {
+                L2_PUT(e_ & 0xFFu, 8u);
+                const uint32_t U_ = E_USED(e_);
+                bb <<= U_;
+                nb -= U_;
+                rem -= U_;
+                L2_REFILL();
+              }
+            }
+          }
+          run = run && !failed && !stopf && rem >= G2;
+        }
+        DLS(3);
+      }
+#undef L2_REFILL
+      store_service(act && (P >> 9) > st, true);  // (room for the careful steps' bytes)
+      prefetch(mn);  // the next group's first blocks, in flight over this one's tail
+      // ---- careful steps: the last < 2 LB bits (or a long code at the tail)
+      uint32_t t_bits = 0, t_win = 0;
+      bool done = !act || failed;
+      while (__ballot(!done)) {
+        const uint32_t w = (uint32_t)(bb >> 32);
+        const bool stop = done || rem == 0u;
+        uint32_t e = T.lut[w >> (32 - LB)];
+        const bool slow = e == 0u && !stop;
+        if (__ballot(slow)) {
+          if (slow) e = slow_entry(T, w, rem);
+        }
+        const bool eos = e == 0xFFFFFFFFu && !stop;
+        const uint32_t L1 = E_L1(e), U = E_USED(e);
+        const bool take1 = !stop && !eos && L1 <= rem;
+        const bool take2 = take1 && E_CNT(e) == 2u && U <= rem;
+        const bool tail = !stop && !eos && !take1;
+        t_bits = tail ? rem : t_bits;
+        t_win = tail ? w : t_win;
+        const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
+        if (take1) L2_PUT(e & (take2 ? 0xFFFFu : 0xFFu), take2 ? 16u : 8u);
+        bb <<= adv;
+        rem -= adv;
+        failed = failed || eos;
+        done = done || eos || !take1 || rem == 0u;
+      }
+#undef L2_PUT
+      DLS(4);
+      // ---- the rest of the output: every block with a decoded byte, whole
+      while (__ballot(act && P > 512u * st)) store_service(act && P > 512u * st, true);
+      if (have) {
+        if (bad) {
+          status[i] = NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+          if (fstate_out) {
+            fstate_out[i] = 0u;
+            flags_out[i] = 0u;
+          }
+        } else {
+          dd_finish(T, failed, t_bits, t_win, P >> 3, slot_ovf, i, status, fstate_out, flags_out);
+        }
+      }
+      g = gn;
+      DLS(5);
+    }
+  }
+  DLS_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -4013,6 +4492,21 @@ static int decode_lanes(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   return hip_rv(hipGetLastError());
 }
 
+static int decode_lanes2(const uint8_t *src, const uint32_t *src_off, uint32_t n, uint8_t *dst,
+                         size_t dst_cap, uint32_t *dst_off, int32_t *status, uint16_t *fstate,
+                         uint8_t *flags, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
+  if (!src || !src_off || !dst || !status) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  const uint32_t grid = persistent_grid<k_decode_lanes2, L2_NT, 64>(n);
+  hipLaunchKernelGGL(k_decode_lanes2, dim3(grid), dim3(L2_NT), 0, st, src, src_off, n, dst,
+                     (uint64_t)dst_cap, dst_off, status, fstate, flags);
+  return hip_rv(hipGetLastError());
+}
+
 extern "C" {
 
 // Lane decoder, A/B entry: mode bit 0 = the caller's slots (decode_batch
@@ -4023,6 +4517,8 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__decode_batch_lanes(const uint8_t *src, co
                                                           uint16_t *fstate, uint8_t *flags,
                                                           void *stream, int mode) {
   const bool sort = !(mode & 2);
+  if (mode & 4)
+    return decode_lanes2(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, stream);
   if (mode & 1)
     return decode_lanes<false>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags,
                                stream, sort);

@@ -10,6 +10,7 @@ import torch
 import nghttp2_amd
 from nghttp2_amd import hd, workloads as W
 dev = torch.device("cuda:0")
+MODE = int(os.environ.get("DL_MODE", "0"))  # 4: the cooperative-transfer decoder
 vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
 P = lambda t: ctypes.c_void_p(t.data_ptr())
 libs = {"base": hd.lib()}
@@ -27,7 +28,7 @@ for cfg in [int(x) for x in sys.argv[1].split(",")]:
         src = torch.from_numpy(pool).to(dev); so = torch.from_numpy(off.view(np.int32)).to(dev)
         enc, eo = codec.encode(src, so, raw_bytes=int(off[-1]))
     torch.cuda.synchronize()
-    n = eo.numel() - 1; E = int(eo[-1].item()); cap = (E * 8) // 5 + 16 * n + 32
+    n = eo.numel() - 1; E = int(eo[-1].item()); cap = 64 * ((((E * 8) // 5) + 63) // 64 + n) + 64
     d = torch.empty(cap, dtype=torch.uint8, device=dev)
     do = torch.empty(n + 1, dtype=torch.int32, device=dev)
     st = torch.empty(n, dtype=torch.int32, device=dev)
@@ -38,7 +39,7 @@ for cfg in [int(x) for x in sys.argv[1].split(",")]:
             a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
             a.record(s)
             rv = L.nghttp2_amd_hd__decode_batch_lanes(P(enc), P(eo), n, P(d), cap, P(do), P(st), None, None,
-                                                      ctypes.c_void_p(s.cuda_stream), 0)
+                                                      ctypes.c_void_p(s.cuda_stream), MODE)
             b.record(s); torch.cuda.synchronize()
             assert rv == 0
             if it >= 2: res[k].append(a.elapsed_time(b) * 1000)

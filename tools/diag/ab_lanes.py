@@ -62,6 +62,7 @@ def main():
         bufs["items"] = mk(capA)
         bufs["lanes"] = mk(capL)
         bufs["lanes_nosort"] = mk(capL)
+        bufs["lanes2"] = mk(64 * ((((E * 8) // 5) + 63) // 64 + n))
         bufs["lanes_exact"] = mk(int(rdo[-1]) + 16)
         bufs["lanes_exact"][1].copy_(exact_off)
 
@@ -72,7 +73,7 @@ def main():
                 rv = L.nghttp2_amd_hd_huff_decode_batch_auto(P(enc), P(eo), n, P(d), d.numel(), P(do),
                                                              P(st), f1, f2, ctypes.c_void_p(s.cuda_stream))
             else:
-                mode = {"lanes": 0, "lanes_nosort": 2, "lanes_exact": 1}[k]
+                mode = {"lanes": 0, "lanes_nosort": 2, "lanes_exact": 1, "lanes2": 4}[k]
                 rv = L.nghttp2_amd_hd__decode_batch_lanes(P(enc), P(eo), n, P(d), d.numel(), P(do),
                                                           P(st), f1, f2,
                                                           ctypes.c_void_p(s.cuda_stream), mode)
@@ -94,7 +95,7 @@ def main():
             i = int(np.nonzero(d[:int(rdo[-1])] != rd[:int(rdo[-1])])[0][0])
             res["exact_first_bad_byte"] = i
             res["exact_first_bad_str"] = int(np.searchsorted(rdo, i, side="right") - 1)
-        for k in ("lanes", "lanes_nosort"):
+        for k in ("lanes", "lanes_nosort", "lanes2"):
             d2, do2, st2, fs2, fl2 = [x.cpu().numpy() for x in bufs[k]]
             ok = np.array_equal(st2, rst) and np.array_equal(fs2.view(np.uint16), rfs) and \
                 np.array_equal(fl2, rfl)

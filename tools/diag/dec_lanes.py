@@ -11,7 +11,7 @@ import nghttp2_amd
 from nghttp2_amd import hd, workloads as W
 
 cfg, reps = int(sys.argv[1]), int(sys.argv[2])
-mode = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+mode = int(sys.argv[3]) if len(sys.argv) > 3 else int(os.environ.get("DL_MODE", "0"))
 dev = torch.device("cuda:0")
 vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
 L = hd.lib()
@@ -29,7 +29,7 @@ else:
 torch.cuda.synchronize()
 n = eo.numel() - 1
 E = int(eo[-1].item())
-cap = (E * 8) // 5 + 16 * n + 32
+cap = 64 * ((((E * 8) // 5) + 63) // 64 + n) + 64
 d = torch.empty(cap, dtype=torch.uint8, device=dev)
 do = torch.empty(n + 1, dtype=torch.int32, device=dev)
 st = torch.empty(n, dtype=torch.int32, device=dev)

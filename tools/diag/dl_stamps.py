@@ -20,7 +20,7 @@ L.nghttp2_amd_hd__decode_batch_lanes.argtypes = [vp, vp, u32, vp, sz, vp, vp, vp
 L.nghttp2_amd_hd__dl_stamps.argtypes = [vp, ctypes.c_int]
 codec = nghttp2_amd.HuffmanBatchCodec(dev)
 for cfg in [int(x) for x in sys.argv[1:]] or [3, 2]:
-    for mode in (0, 2):
+    for mode in [int(x) for x in os.environ.get("DL_MODES", "0,2").split(",")]:
         pool, off = W.gen_pseudo_headers(1 << 20) if cfg == 2 else W.gen_mixed_values(1 << 20)
         src = torch.from_numpy(pool).to(dev)
         so = torch.from_numpy(off.view(np.int32)).to(dev)
@@ -28,7 +28,7 @@ for cfg in [int(x) for x in sys.argv[1:]] or [3, 2]:
         torch.cuda.synchronize()
         n = eo.numel() - 1
         E = int(eo[-1].item())
-        cap = (E * 8) // 5 + 16 * n + 32
+        cap = 64 * ((((E * 8) // 5) + 63) // 64 + n) + 64
         d = torch.empty(cap, dtype=torch.uint8, device=dev)
         do = torch.empty(n + 1, dtype=torch.int32, device=dev)
         st = torch.empty(n, dtype=torch.int32, device=dev)
