@@ -51,8 +51,8 @@ extern "C" {
 
 /* dst_off[n] after nghttp2_amd_hd_huff_encode_batch when the batch's encoded
  * total does not fit min(dst_cap, 0xFFFFFFFE): offsets are uint32, so such a
- * batch must be split (no offset of it is valid, no byte was written past
- * dst_cap). */
+ * batch must be split (no offset of it is valid, no byte was written at or
+ * past dst_cap). */
 #define NGHTTP2_AMD_OFF_OVERFLOW 0xFFFFFFFFu
 
 /* Decode-context flag bits (lib/nghttp2_hd_huffman.h:35-37). */
@@ -116,10 +116,14 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw
  * (all ones) padding of the last byte.  Size dst_cap by
  * nghttp2_amd_hd_huff_encode_bound(src_off[n]-src_off[0], n); the kernels
  * never write past dst_cap.  Offsets are uint32: when the encoded total
- * would pass min(dst_cap, 0xFFFFFFFE) the batch writes no bytes and
- * dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW (check it after the stream
- * synchronises; split the batch).
+ * would pass min(dst_cap, 0xFFFFFFFE), dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW
+ * (check it after the stream synchronises) and the batch must be split: the
+ * tiles of 256 strings that fit may already be written, nothing at or past
+ * dst_cap is, and no offset of the batch is valid.  A batch holding a
+ * string longer than NGHTTP2_AMD_ENCODE_MAX_STRING raw bytes (its code bits
+ * would not fit the kernels' 32-bit counts) is marked the same way.
  */
+#define NGHTTP2_AMD_ENCODE_MAX_STRING (0xFFFFFFFFu / 30u)
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst, size_t dst_cap,
                                      uint32_t *dst_off, void *workspace,
@@ -216,10 +220,17 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, cons
  * strings and writes nothing for them.  Offsets
  * are uint32: dst_cap > 0xFFFFFFFF returns NGHTTP2_AMD_ERR_INVALID_ARGUMENT
  * (split a batch whose decode_bound passes 4 GiB).
+ *
+ * enc_bytes is the batch's encoded size, src_off[n] - src_off[0] (the value
+ * that sized dst by nghttp2_amd_hd_huff_decode_bound).  It only picks the
+ * kernel instance: a mean of at most 48 bytes per string (header-sized
+ * strings) decodes whole strings as 64-byte items, a larger one cuts strings
+ * into 40-byte pieces.  Both are exact for any input, so a wrong value costs
+ * time, never correctness.  dst_cap does not enter the pick.
  */
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
-                                          uint32_t n, uint8_t *dst, size_t dst_cap,
-                                          uint32_t *dst_off, int32_t *status,
+                                          uint32_t n, uint64_t enc_bytes, uint8_t *dst,
+                                          size_t dst_cap, uint32_t *dst_off, int32_t *status,
                                           uint16_t *fstate, uint8_t *flags, void *stream);
 
 /*

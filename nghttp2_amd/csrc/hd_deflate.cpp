@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/nghttp2_amd_hd.h"
+#include "../../include/nghttp2_amd_hd_testing.h"
 #include "host_threads.h"
 #include "hd_tokens.h"
 
@@ -193,9 +194,9 @@ struct Piece {
 
 extern "C" {
 
-NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__test_fail_deflate_gpu(int n) { g_fail_gpu.store(n); }
-// (tests, A/B) the batch size from which field names go through the GPU
-NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__set_gpu_names_min(uint32_t n) { g_names_min.store(n); }
+// test hooks (include/nghttp2_amd_hd_testing.h)
+void nghttp2_amd_hd__test_fail_deflate_gpu(int n) { g_fail_gpu.store(n); }
+void nghttp2_amd_hd__set_gpu_names_min(uint32_t n) { g_names_min.store(n); }
 
 int nghttp2_amd_hd_deflate_new(nghttp2_amd_hd_deflater **deflater_ptr,
                                size_t max_deflate_dynamic_table_size) {

@@ -517,8 +517,9 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
         hipMemcpyAsync(E.d_off, E.h_meta, (nh + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
                        st) != hipSuccess)
       return NGHTTP2_AMD_ERR_FATAL;
-    int rv = nghttp2_amd_hd_huff_decode_batch_auto(E.d_in, E.d_off, nh, E.d_out, out_bytes,
-                                                   E.d_slot, E.d_st, nullptr, nullptr, stream);
+    int rv = nghttp2_amd_hd_huff_decode_batch_auto(E.d_in, E.d_off, nh, (uint64_t)hoff[nh], E.d_out,
+                                                   out_bytes, E.d_slot, E.d_st, nullptr, nullptr,
+                                                   stream);
     if (rv) return rv;
     uint32_t *h_slot = E.h_meta + (nh + 1);
     int32_t *h_st = (int32_t *)(h_slot + (nh + 1));

@@ -29,15 +29,6 @@ namespace {
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 constexpr uint32_t NT_WG = 256;
-#ifndef NAMES_BAL
-// 1: byte-balanced lanes (k_name_tokens_bal).  Measured slower on both
-// batches (1M mixed names 116.5 vs 38.7 us, 1M short names 33.0 vs 26.4 us,
-// tools/diag/ab_names.py): one dword per dependent loop iteration exposes the
-// load latency that the per-name layout hides with a chunk in flight, and the
-// long names of the mixed batch come in whole waves, where one lane per name
-// is already balanced.  Kept as the A/B alternative.
-#define NAMES_BAL 0
-#endif
 
 __constant__ hdtok::Table kTokTable = hdtok::kTable;
 
@@ -141,143 +132,6 @@ __global__ __launch_bounds__(NT_WG) void k_name_tokens(const uint8_t *__restrict
   hash[s] = h;
 }
 
-// ---------------------------------------------------------------------------
-// Byte-balanced layout (A/B alternative, NAMES_BAL).  A wave takes NB_K consecutive
-// names and splits their contiguous bytes [A, Z) into 64 equal slices: lane l
-// hashes the names that start in slice l, one after another, ONE DWORD PER
-// LOOP ITERATION whatever name it belongs to -- so every lane runs about
-// (Z - A) / 256 + (its names) iterations and a wave's cost follows its bytes,
-// not its longest name (one lane per name wasted ~78 % of its FNV steps on
-// the mixed batch).  A name's hash is stored when its last dword is done;
-// the tokens follow in a second phase, one lane per name, as above.
-// ---------------------------------------------------------------------------
-constexpr uint32_t NB_K = 256;  // names per wave
-
-__device__ __forceinline__ int32_t probe_token(const lds_u32 *TH, const lds_u32 *TM,
-                                               const lds_u32 *TN, const uint8_t *names,
-                                               uint32_t a, uint32_t len, uint32_t h) {
-  if (len > 32u) return -1;
-  // the first slot whose hash and length match, then the bytes
-  uint32_t slot = h & (hdtok::kSlots - 1u), m = 0;
-  for (uint32_t k = 0; k < hdtok::kSlots; ++k, slot = (slot + 1u) & (hdtok::kSlots - 1u)) {
-    m = TM[slot];
-    if (m == 0 || (TH[slot] == h && hdtok::meta_len(m) == len)) break;
-  }
-  if (m == 0) return -1;
-  const uint32_t *g = reinterpret_cast<const uint32_t *>(names + (a & ~3u));
-  const uint32_t sh = a & 3u;
-  uint32_t prev = g[0];
-  bool eq = true;
-#pragma unroll
-  for (uint32_t i = 0; i < 8u; ++i) {
-    if (4u * i >= len) break;
-    const uint32_t nxt = g[i + 1u];
-    uint32_t v = __builtin_amdgcn_alignbyte(nxt, prev, sh);
-    const uint32_t left = len - 4u * i;
-    if (left < 4u) v &= (1u << (8u * left)) - 1u;
-    eq = eq && v == TN[(hdtok::meta_off(m) >> 2) + i];
-    prev = nxt;
-  }
-  // (a hash and length match whose bytes differ: keep probing)
-  if (eq) return (int32_t)hdtok::meta_token(m);
-  for (uint32_t k = 0; k < hdtok::kSlots; ++k) {
-    slot = (slot + 1u) & (hdtok::kSlots - 1u);
-    m = TM[slot];
-    if (m == 0) return -1;
-    if (TH[slot] != h || hdtok::meta_len(m) != len) continue;
-    prev = g[0];
-    eq = true;
-    for (uint32_t i = 0; i < 8u && 4u * i < len; ++i) {
-      const uint32_t nxt = g[i + 1u];
-      uint32_t v = __builtin_amdgcn_alignbyte(nxt, prev, sh);
-      const uint32_t left = len - 4u * i;
-      if (left < 4u) v &= (1u << (8u * left)) - 1u;
-      eq = eq && v == TN[(hdtok::meta_off(m) >> 2) + i];
-      prev = nxt;
-    }
-    if (eq) return (int32_t)hdtok::meta_token(m);
-  }
-  return -1;
-}
-
-__global__ __launch_bounds__(NT_WG) void k_name_tokens_bal(const uint8_t *__restrict__ names,
-                                                           const uint32_t *__restrict__ off,
-                                                           uint32_t n, int32_t *__restrict__ token,
-                                                           uint32_t *__restrict__ hash) {
-  __shared__ uint32_t th[hdtok::kSlots], tm[hdtok::kSlots];
-  __shared__ uint32_t tn[hdtok::kNameBytes / 4];
-  __shared__ uint32_t so[NT_WG / 64][NB_K + 1];
-  __shared__ uint32_t sh[NT_WG / 64][NB_K];  // the names' hashes
-  for (uint32_t i = threadIdx.x; i < hdtok::kSlots; i += NT_WG) {
-    th[i] = kTokTable.hash[i];
-    tm[i] = kTokTable.meta[i];
-  }
-  for (uint32_t i = threadIdx.x; i < hdtok::kNameBytes / 4; i += NT_WG)
-    tn[i] = reinterpret_cast<const uint32_t *>(kTokTable.names)[i];
-  __syncthreads();  // the only workgroup barrier
-  const lds_u32 *TH = (const lds_u32 *)th, *TM = (const lds_u32 *)tm, *TN = (const lds_u32 *)tn;
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t n0 = (blockIdx.x * (NT_WG / 64) + wv) * NB_K;
-  if (n0 >= n) return;
-  const uint32_t cnt = min(NB_K, n - n0);
-  lds_u32 *O = (lds_u32 *)so[wv];
-  lds_u32 *H = (lds_u32 *)sh[wv];
-  for (uint32_t i = lane; i <= cnt; i += 64u) O[i] = off[n0 + i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t A = O[0], Z = O[cnt];
-  const uint32_t slice = max(1u, (Z - A + 63u) / 64u);
-  // names starting in [A + lane*slice, A + (lane+1)*slice) (the last lane:
-  // through the end, empty names at Z included): lower bounds over O
-  auto lower = [&](uint32_t x) {  // first i in [0, cnt] with O[i] >= x
-    uint32_t lo = 0, hi = cnt;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (O[mid] < x) lo = mid + 1u; else hi = mid;
-    }
-    return lo;
-  };
-  uint32_t ci = lane == 0 ? 0u : lower(A + lane * slice);
-  const uint32_t ce = lane == 63u ? cnt : lower(A + (lane + 1u) * slice);
-  // one dword per iteration: name ci's bytes [ca, cb), dword at p
-  uint32_t ca = ci < ce ? O[ci] : 0u, cb = ci < ce ? O[ci + 1u] : 0u;
-  uint32_t p = ca & ~3u, h = hdtok::kFnvBasis;
-  while (__ballot(ci < ce)) {
-    if (ci < ce) {
-      if (p < cb) {
-        const uint32_t w = *reinterpret_cast<const uint32_t *>(names + p);
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k) {
-          const uint32_t c = (w >> (8u * k)) & 0xFFu;
-          const uint32_t hn = (h ^ c) * hdtok::kFnvPrime;
-          h = (p + k >= ca && p + k < cb) ? hn : h;
-        }
-        p += 4u;
-      }
-      if (p >= cb) {  // the name is done (an empty one at once)
-        H[ci] = h;
-        ++ci;
-        h = hdtok::kFnvBasis;
-        if (ci < ce) {
-          ca = cb;
-          cb = O[ci + 1u];
-          p = ca & ~3u;
-        }
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // hashes out and tokens: one lane per name
-  for (uint32_t i = lane; i < cnt; i += 64u) {
-    const uint32_t a = O[i], len = O[i + 1u] - a, hi = H[i];
-    hash[n0 + i] = hi;
-    token[n0 + i] = len <= 32u ? probe_token(TH, TM, TN, names, a, len, hi) : -1;
-  }
-}
-
 }  // namespace
 
 extern "C" {
@@ -286,12 +140,8 @@ int nghttp2_amd_hd_name_tokens_batch(const uint8_t *names, const uint32_t *name_
                                      int32_t *token, uint32_t *hash, void *stream) {
   if (n == 0) return 0;
   if (!names || !name_off || !token || !hash) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if (NAMES_BAL)
-    hipLaunchKernelGGL(k_name_tokens_bal, dim3((n + NT_WG / 64u * NB_K - 1u) / (NT_WG / 64u * NB_K)),
-                       dim3(NT_WG), 0, (hipStream_t)stream, names, name_off, n, token, hash);
-  else
-    hipLaunchKernelGGL(k_name_tokens, dim3((n + NT_WG - 1u) / NT_WG), dim3(NT_WG), 0,
-                       (hipStream_t)stream, names, name_off, n, token, hash);
+  hipLaunchKernelGGL(k_name_tokens, dim3((n + NT_WG - 1u) / NT_WG), dim3(NT_WG), 0,
+                     (hipStream_t)stream, names, name_off, n, token, hash);
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess) return 0;
   fprintf(stderr, "nghttp2_amd_hd: HIP error %s\n", hipGetErrorString(e));

@@ -67,13 +67,11 @@ def lib():
         L.nghttp2_amd_hd_huff_decode_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, vp]
         L.nghttp2_amd_hd_huff_decode_bound.restype = sz
         L.nghttp2_amd_hd_huff_decode_bound.argtypes = [ctypes.c_uint64, u32]
-        L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, u32, vp, sz, vp, vp, vp,
-                                                            vp, vp]
+        u64 = ctypes.c_uint64
+        L.nghttp2_amd_hd_huff_decode_batch_auto.argtypes = [vp, vp, u32, u64, vp, sz, vp, vp,
+                                                            vp, vp, vp]
         L.nghttp2_amd_hd_huff_decode_fsm_batch.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp,
                                                            vp, vp, ctypes.c_int, vp]
-        L.nghttp2_amd_hd__decode_batch_items.argtypes = [vp, vp, u32, vp, sz, vp, vp, vp,
-                                                         vp, vp, ctypes.c_int]
-        u64 = ctypes.c_uint64
         L.nghttp2_amd_hd_emit_strings_bound.restype = sz
         L.nghttp2_amd_hd_emit_strings_bound.argtypes = [u64, u32]
         L.nghttp2_amd_hd_emit_strings_workspace_size.restype = sz
@@ -126,8 +124,12 @@ def _stream(stream):
 class HuffmanBatchCodec:
     """Batched HPACK Huffman codec on one device.
 
-    Keeps a workspace sized for the largest batch seen; all calls are
-    asynchronous on the given (default: current) torch stream.
+    All calls are asynchronous on the given (default: current) torch stream.
+    A codec may be used from several streams: each stream gets its own device
+    workspaces (tile sums, the framing pool), allocated on that stream and
+    grown there, so calls on different streams never share scratch and a
+    regrown block is only reused in the order of its own stream.  Calls on one
+    stream run in issue order, as any work on a stream does.
     """
 
     def __init__(self, device=None):
@@ -135,20 +137,34 @@ class HuffmanBatchCodec:
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
         self.L = lib()
-        self._ws = None
-        self._ews = None
+        self._scratch = {}  # (stream handle, kind) -> uint8 tensor allocated on that stream
+
+    def _on(self, stream):
+        return stream if stream is not None else self.torch.cuda.current_stream(self.device)
+
+    def _scratch_for(self, kind, need, stream):
+        s = self._on(stream)
+        key = (s.cuda_stream, kind)
+        t = self._scratch.get(key)
+        if t is None or t.numel() < need:
+            # Uninitialised on purpose: the kernels write every scratch word
+            # they read (a zero fill would be one more kernel).  Allocated
+            # under the call's own stream, so the caching allocator ties the
+            # block to it.
+            with self.torch.cuda.stream(s):
+                t = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
+            self._scratch[key] = t
+        return t
+
+    def _empty(self, n, dtype, stream):
+        """An output tensor allocated under the call's stream (so the caching
+        allocator never hands its block to another stream while the call's
+        kernels may still write it)."""
+        with self.torch.cuda.stream(self._on(stream)):
+            return self.torch.empty(n, dtype=dtype, device=self.device)
 
     def _workspace(self, n, raw_bytes=None, stream=None):
-        need = self.L.nghttp2_amd_hd_huff_workspace_size(n)
-        if self._ws is None or self._ws.numel() < need:
-            # Uninitialised on purpose: the kernels write every workspace word
-            # they read.  (A zero fill would be a kernel on the *current*
-            # stream, unordered with a call on another stream: it once
-            # overwrote a running encode's tile sums in the two-stream bench.)
-            with self.torch.cuda.stream(stream if stream is not None
-                                        else self.torch.cuda.current_stream(self.device)):
-                self._ws = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
-        return self._ws
+        return self._scratch_for("ws", self.L.nghttp2_amd_hd_huff_workspace_size(n), stream)
 
     def encode_bound(self, raw_bytes, n):
         return self.L.nghttp2_amd_hd_huff_encode_bound(int(raw_bytes), int(n))
@@ -161,9 +177,9 @@ class HuffmanBatchCodec:
             raw_bytes = src.numel()
         cap = self.encode_bound(raw_bytes, n)
         if dst is None:
-            dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            dst = self._empty(cap, torch.uint8, stream)
         if dst_off is None:
-            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+            dst_off = self._empty(n + 1, torch.int32, stream)
         ws = self._workspace(n, raw_bytes, stream)
         rv = self.L.nghttp2_amd_hd_huff_encode_batch(
             _p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(ws),
@@ -174,7 +190,7 @@ class HuffmanBatchCodec:
     def encode_count(self, src, src_off, enc_len=None, stream=None):
         n = src_off.numel() - 1
         if enc_len is None:
-            enc_len = self.torch.empty(max(1, n), dtype=self.torch.int32, device=self.device)
+            enc_len = self._empty(max(1, n), self.torch.int32, stream)
         rv = self.L.nghttp2_amd_hd_huff_encode_count_batch(
             _p(src), _p(src_off), n, _p(enc_len), _stream(stream))
         _check(rv, "encode_count_batch")
@@ -187,9 +203,9 @@ class HuffmanBatchCodec:
         torch = self.torch
         n = name_off.numel() - 1
         if token is None:
-            token = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+            token = self._empty(max(1, n), torch.int32, stream)
         if hash is None:
-            hash = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+            hash = self._empty(max(1, n), torch.int32, stream)
         rv = self.L.nghttp2_amd_hd_name_tokens_batch(
             _p(names), _p(name_off), n, _p(token), _p(hash), _stream(stream))
         _check(rv, "name_tokens_batch")
@@ -205,22 +221,23 @@ class HuffmanBatchCodec:
             raw_bytes = src.numel()
         cap = self.L.nghttp2_amd_hd_emit_strings_bound(int(raw_bytes), n)
         if dst is None:
-            dst = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            dst = self._empty(cap, torch.uint8, stream)
         if dst_off is None:
-            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+            dst_off = self._empty(n + 1, torch.int32, stream)
         need = self.L.nghttp2_amd_hd_emit_strings_workspace_size(int(raw_bytes), n)
-        if self._ews is None or self._ews.numel() < need:
-            self._ews = torch.empty(need, dtype=torch.uint8, device=self.device)
+        ews = self._scratch_for("ews", need + 256, stream)
+        base = (256 - ews.data_ptr() % 256) % 256  # (the API wants it 256-byte aligned)
+        ews = ews[base:base + need]
         rv = self.L.nghttp2_amd_hd_emit_strings_batch(
             _p(src), _p(src_off), n, int(raw_bytes), _p(dst), dst.numel(), _p(dst_off),
-            _p(self._ews), self._ews.numel(), _stream(stream))
+            _p(ews), ews.numel(), _stream(stream))
         _check(rv, "emit_strings_batch")
         return dst, dst_off
 
     def decode_slots(self, src_off, dst_off=None, stream=None):
         n = src_off.numel() - 1
         if dst_off is None:
-            dst_off = self.torch.empty(n + 1, dtype=self.torch.int32, device=self.device)
+            dst_off = self._empty(n + 1, self.torch.int32, stream)
         ws = self._workspace(n, stream=stream)
         rv = self.L.nghttp2_amd_hd_huff_decode_slots(
             _p(src_off), n, _p(dst_off), _p(ws), ws.numel(), _stream(stream))
@@ -231,34 +248,32 @@ class HuffmanBatchCodec:
         return self.L.nghttp2_amd_hd_huff_decode_bound(int(enc_bytes), int(n))
 
     def decode_auto(self, src, src_off, enc_bytes=None, dst=None, dst_off=None, status=None,
-                    want_ctx=False, stream=None, piece=0):
+                    want_ctx=False, stream=None, pick=None):
         """Decode into a dense pool (one launch): the strings of each task of
         64 consecutive strings back to back from the task's base
-        auto_slot(x_t0, t0).  piece = 64 / 40 / 32 forces an instance of the
-        item decoder, 66..69 a budgeted-round instance (tests, A/B); 0 lets
-        the library pick.  Returns
+        auto_slot(x_t0, t0).  enc_bytes = src_off[n] - src_off[0] (default: the
+        pool size, an upper bound) sizes dst and picks the kernel instance by
+        the mean string length; pick = "items64" / "pieces40" forces one
+        instance through that same argument (tests).  Returns
         (dst, dst_off, status[, fstate, flags])."""
         torch = self.torch
         n = src_off.numel() - 1
         if enc_bytes is None:
             enc_bytes = src.numel()
+        sel = {None: int(enc_bytes), "items64": 0, "pieces40": 49 * max(1, n)}[pick]
         if dst is None:
-            dst = torch.empty(self.decode_bound(enc_bytes, n), dtype=torch.uint8,
-                              device=self.device)
+            dst = self._empty(self.decode_bound(enc_bytes, n), torch.uint8, stream)
         if dst_off is None:
-            dst_off = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+            dst_off = self._empty(n + 1, torch.int32, stream)
         if status is None:
-            status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+            status = self._empty(max(1, n), torch.int32, stream)
         fstate = flags = None
         if want_ctx:
-            fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
-            flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
-        args = (_p(src), _p(src_off), n, _p(dst), dst.numel(), _p(dst_off), _p(status),
-                _p(fstate), _p(flags), _stream(stream))
-        if piece:
-            rv = self.L.nghttp2_amd_hd__decode_batch_items(*args, piece)
-        else:
-            rv = self.L.nghttp2_amd_hd_huff_decode_batch_auto(*args)
+            fstate = self._empty(max(1, n), torch.int16, stream)
+            flags = self._empty(max(1, n), torch.uint8, stream)
+        rv = self.L.nghttp2_amd_hd_huff_decode_batch_auto(
+            _p(src), _p(src_off), n, sel, _p(dst), dst.numel(), _p(dst_off), _p(status),
+            _p(fstate), _p(flags), _stream(stream))
         _check(rv, "decode_batch_auto")
         if want_ctx:
             return dst, dst_off, status[:n], fstate[:n], flags[:n]
@@ -270,9 +285,9 @@ class HuffmanBatchCodec:
         (status, fstate, flags)."""
         torch = self.torch
         n = src_off.numel() - 1
-        status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
-        fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
-        flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        status = self._empty(max(1, n), torch.int32, stream)
+        fstate = self._empty(max(1, n), torch.int16, stream)
+        flags = self._empty(max(1, n), torch.uint8, stream)
         rv = self.L.nghttp2_amd_hd_huff_decode_fsm_batch(
             _p(src), _p(src_off), n, _p(dst), _p(dst_off), _p(status), _p(fstate),
             _p(flags), _p(init_fstate), _p(init_flags), 1 if final else 0, _stream(stream))
@@ -295,13 +310,13 @@ class HuffmanBatchCodec:
         if dst is None:
             if dst_cap is None:
                 dst_cap = int(dst_off[-1].item()) + 16
-            dst = torch.empty(dst_cap, dtype=torch.uint8, device=self.device)
+            dst = self._empty(dst_cap, torch.uint8, stream)
         if status is None:
-            status = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+            status = self._empty(max(1, n), torch.int32, stream)
         fstate = flags = None
         if want_ctx:
-            fstate = torch.empty(max(1, n), dtype=torch.int16, device=self.device)
-            flags = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+            fstate = self._empty(max(1, n), torch.int16, stream)
+            flags = self._empty(max(1, n), torch.uint8, stream)
         rv = self.L.nghttp2_amd_hd_huff_decode_batch(
             _p(src), _p(src_off), n, _p(dst), _p(dst_off), _p(status), _p(fstate),
             _p(flags), _stream(stream))

@@ -45,6 +45,16 @@ def test_library_exports_every_declared_symbol():
         getattr(L, n)
 
 
+def test_library_exports_nothing_else():
+    """The dynamic symbol table is exactly the declared C ABI: no kernel
+    stubs, template instantiations or retired A/B entry points."""
+    import nghttp2_amd
+    out = subprocess.run(["nm", "-D", "--defined-only", nghttp2_amd.lib_path()], check=True,
+                         capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    assert exported == set(declared_functions()), sorted(exported ^ set(declared_functions()))
+
+
 def test_library_is_gfx950_code_object():
     """The .so carries a HIP fat binary with a gfx950 code object."""
     import nghttp2_amd

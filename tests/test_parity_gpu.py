@@ -250,10 +250,10 @@ def _variant_inputs():
     yield "mixed", e3, eo3
 
 
-@pytest.mark.parametrize("variant", ["auto", "items64", "items66", "items67", "items68", "items69", "items40", "items32", "fsm"])
+@pytest.mark.parametrize("variant", ["auto", "items64", "pieces40", "fsm"])
 def test_decode_variants_match_oracle(codec, dev, variant):
-    """decode_batch_auto (dense item decoder: the library's pick and every
-    instance) and the batched reference FSM kernel agree with the oracle on
+    """decode_batch_auto (dense item decoder: the library's pick and both
+    instances) and the batched reference FSM kernel agree with the oracle on
     status, final context and every written byte."""
     import torch
     for tag, enc, eoff in _variant_inputs():
@@ -264,8 +264,9 @@ def test_decode_variants_match_oracle(codec, dev, variant):
         if variant != "fsm":
             cap = codec.decode_bound(int(eoff[-1]), n)
             dst = torch.zeros(cap, dtype=torch.uint8, device=dev)
-            piece = 0 if variant == "auto" else int(variant[5:])
-            dst, do, st, fs, fl = codec.decode_auto(src, so, dst=dst, want_ctx=True, piece=piece)
+            pick = None if variant == "auto" else variant
+            dst, do, st, fs, fl = codec.decode_auto(src, so, enc_bytes=int(eoff[-1]), dst=dst,
+                                                    want_ctx=True, pick=pick)
             do = do.cpu().numpy().view(np.uint32)
             check_dense_layout(dst.cpu().numpy(), do, enc, eoff, tag)
         else:
@@ -382,8 +383,8 @@ def test_emit_strings_parity(codec, dev, kind):
     check_emit(codec, dev, pool, off, kind)
 
 
-@pytest.mark.parametrize("piece", [0, 64, 66, 67, 68, 69, 40, 32])
-def test_dense_decode_edges(codec, dev, piece):
+@pytest.mark.parametrize("pick", [None, "items64", "pieces40"])
+def test_dense_decode_edges(codec, dev, pick):
     """decode_batch_auto (each item-decoder instance) on strings that stress
     its pieces:
     ends on and near piece and round boundaries, runs of empty strings (also
@@ -410,8 +411,8 @@ def test_dense_decode_edges(codec, dev, piece):
         n = len(eo) - 1
         src = to_dev(pad16(e, eo[-1]), dev)
         dst = torch.zeros(codec.decode_bound(int(eo[-1]), n), dtype=torch.uint8, device=dev)
-        dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eo, dev), dst=dst, want_ctx=True,
-                                                piece=piece)
+        dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eo, dev), enc_bytes=int(eo[-1]),
+                                                dst=dst, want_ctx=True, pick=pick)
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), rst), tag
         assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag
@@ -437,3 +438,153 @@ def test_decode_descending_offsets_refused(codec, dev):
     assert (st[64:128] == -501).all()
     rst = O.decode_batch(enc, eoff)[2]
     assert np.array_equal(st[:64], rst[:64]) and np.array_equal(st[128:], rst[128:])
+
+
+# ---- decode_batch_auto (the bench-timed path) under the same parity bar ----
+def auto_decode_check(codec, dev, enc, eoff, tag, pick=None, nthreads=1):
+    """decode_auto vs the oracle: status, {fstate, flags}, and every byte the
+    reference writes for each string (its partial output on failure too),
+    gathered from the dense layout."""
+    import torch
+    n = len(eoff) - 1
+    E = int(eoff[-1])
+    src = to_dev(pad16(enc, E), dev)
+    dst = torch.zeros(codec.decode_bound(E, n), dtype=torch.uint8, device=dev)
+    dst, do, st, fs, fl = codec.decode_auto(src, to_dev(eoff, dev), enc_bytes=E, dst=dst,
+                                            want_ctx=True, pick=pick)
+    torch.cuda.synchronize()
+    rd, rdo, rst, rfs, rfl = O.decode_batch(enc, eoff, nthreads=nthreads)
+    st = st.cpu().numpy()
+    bad = np.nonzero(st != rst)[0]
+    assert bad.size == 0, "%s: status differs at %s (gpu %s, ref %s)" % (
+        tag, bad[:5], st[bad[:5]], rst[bad[:5]])
+    assert np.array_equal(fs.cpu().numpy().view(np.uint16), rfs), tag + ": fstate"
+    assert np.array_equal(fl.cpu().numpy(), rfl), tag + ": flags"
+    # the bytes the oracle wrote per string: its decoded length, or on
+    # failure what it left in the (zero-initialised) slot before the error
+    written = np.where(rst >= 0, rst, 0).astype(np.int64)
+    fail = np.nonzero(rst < 0)[0]
+    for i in fail:
+        _, out, _ = O.decode(bytes(enc[int(eoff[i]):int(eoff[i + 1])]), final=1)
+        written[i] = len(out)
+    d = dst.cpu().numpy()
+    do = do.cpu().numpy().view(np.uint32).astype(np.int64)
+    tot = int(written.sum())
+    rel = np.arange(tot) - np.repeat(np.cumsum(written) - written, written)
+    got = d[np.repeat(do[:-1], written) + rel]
+    want = rd[np.repeat(rdo[:-1].astype(np.int64), written) + rel]
+    if not np.array_equal(got, want):
+        k = int(np.nonzero(got != want)[0][0])
+        i = int(np.searchsorted(np.cumsum(written), k, side="right"))
+        raise AssertionError("%s: decoded byte differs in string %d" % (tag, i))
+    return st, do
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_decode_auto_full_size(codec, dev, cfg):
+    """BASELINE.json configs 2 / 3 at full size (1M strings) through
+    decode_batch_auto with the library's own pick (the instance bench.py
+    times): status, final context and every byte against the oracle."""
+    from nghttp2_amd import workloads as W
+    n = 1 << 20
+    pool, off = W.gen_pseudo_headers(n) if cfg == 2 else W.gen_mixed_values(n)
+    enc, eoff = O.encode_batch(pool, off, nthreads=16)
+    st, do = auto_decode_check(codec, dev, enc, eoff, "config %d" % cfg, nthreads=16)
+    assert np.array_equal(st, np.diff(off.astype(np.int64)))
+
+
+@pytest.mark.parametrize("name", make_golden.CASES)
+def test_decode_auto_golden(codec, dev, name):
+    """The committed golden fixtures through decode_batch_auto."""
+    g = make_golden.load(name)
+    for pick in (None, "items64", "pieces40"):
+        st, _ = auto_decode_check(codec, dev, g["enc"][:int(g["enc_off"][-1])], g["enc_off"],
+                                  name, pick=pick)
+        assert np.array_equal(st, g["status"])
+
+
+def test_decode_auto_max_length_strings(codec, dev):
+    """NGHTTP2_HD_MAX_NV (lib/nghttp2_hd.h:45) sized literals, and longer,
+    through decode_batch_auto: each instance, mixed with short strings."""
+    from nghttp2_amd import workloads as W
+    rng = np.random.default_rng(13)
+    lens = np.array([65536, 1, 70000, 0, 65535, 5, 131072] + [20] * 200, dtype=np.int64)
+    chars = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    pool, off = W._pool_from_lengths(lens, chars)
+    enc, eoff = O.encode_batch(pool, off)
+    for pick in (None, "items64", "pieces40"):
+        st, _ = auto_decode_check(codec, dev, enc, eoff, "max-len %s" % pick, pick=pick)
+        assert np.array_equal(st, lens)
+
+
+@pytest.mark.parametrize("pick", ["items64", "pieces40"])
+def test_decode_auto_small_pool(codec, dev, pick):
+    """A pool smaller than decode_bound: a string whose task span
+    4 (ceil(floor(8 x_{i+1} / 5) / 4) + i + 1) passes dst_cap gets -502, no
+    byte at or past dst_cap is written (guard bytes), dst_off saturates at
+    dst_cap, and every other string is oracle-exact."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_mixed_values(3000, seed=44)
+    enc, eoff = O.encode_batch(pool, off)
+    n = len(eoff) - 1
+    E = int(eoff[-1])
+    bound = codec.decode_bound(E, n)
+    for cut in (700, 300, 37):
+        cap = bound - cut
+        dst = torch.full((bound + 4096,), 0x5A, dtype=torch.uint8, device=dev)
+        src = to_dev(pad16(enc, E), dev)
+        _, do, st, fs, fl = codec.decode_auto(src, to_dev(eoff, dev), enc_bytes=E,
+                                              dst=dst[:cap], want_ctx=True, pick=pick)
+        torch.cuda.synchronize()
+        st = st.cpu().numpy()
+        do = do.cpu().numpy().view(np.uint32).astype(np.int64)
+        d = dst.cpu().numpy()
+        assert (d[cap:] == 0x5A).all(), (pick, cut, "wrote at or past dst_cap")
+        eo = eoff.astype(np.int64)
+        g = (8 * (eo - eo[0])) // 5
+        span_end = 4 * ((g[1:] + 3) // 4 + np.arange(1, n + 1))
+        rd, rdo, rst, rfs, rfl = O.decode_batch(enc, eoff)
+        over = span_end > cap
+        assert over.any() and not over.all()
+        assert (st[over] == O.NGHTTP2_ERR_BUFFER_ERROR).all(), (pick, cut)
+        assert np.array_equal(st[~over], rst[~over]), (pick, cut)
+        assert (do <= cap).all() and do[-1] == min(do[-1], cap)
+        for i in np.nonzero(~over & (rst > 0))[0][::5]:
+            assert bytes(d[do[i]:do[i] + rst[i]]) == bytes(rd[rdo[i]:rdo[i] + rst[i]]), (pick, i)
+
+
+def test_fresh_codec_on_a_side_stream(dev):
+    """A fresh codec whose first encode, emit_strings and decode_auto run on a
+    non-current stream while the current stream is busy: every result equals
+    the oracle (its workspaces are allocated on, and ordered by, the side
+    stream)."""
+    import torch
+    import nghttp2_amd
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_pseudo_headers(40000, seed=61)
+    c = nghttp2_amd.HuffmanBatchCodec(dev)
+    side = torch.cuda.Stream(dev)
+    src = to_dev(pad16(pool, off[-1]), dev)
+    so = to_dev(off, dev)
+    busy = torch.randn(4096, 4096, device=dev)
+    side.wait_stream(torch.cuda.current_stream())  # (the inputs were copied on the current stream)
+    for _ in range(16):
+        busy = busy @ busy * 1e-3  # keeps the current stream busy meanwhile
+    enc, eo = c.encode(src, so, raw_bytes=int(off[-1]), stream=side)
+    lit, lo = c.emit_strings(src, so, raw_bytes=int(off[-1]), stream=side)
+    dst, do, st = c.decode_auto(enc, eo, stream=side)
+    side.synchronize()
+    renc, reoff = O.encode_batch(pool, off)
+    eo_h = eo.cpu().numpy().view(np.uint32)
+    assert np.array_equal(eo_h, reoff)
+    assert np.array_equal(enc.cpu().numpy()[:int(reoff[-1])], renc)
+    rlit, rlo = O.emit_strings_batch(pool, off)
+    assert np.array_equal(lo.cpu().numpy().view(np.uint32), rlo)
+    assert np.array_equal(lit.cpu().numpy()[:int(rlo[-1])], rlit)
+    raw = np.diff(off.astype(np.int64))
+    assert np.array_equal(st.cpu().numpy(), raw)
+    d = dst.cpu().numpy()
+    do = do.cpu().numpy().view(np.uint32).astype(np.int64)
+    rel = np.arange(int(raw.sum())) - np.repeat(np.cumsum(raw) - raw, raw)
+    assert np.array_equal(d[np.repeat(do[:-1], raw) + rel], pool[:int(off[-1])])

@@ -163,8 +163,8 @@ def test_decode_pool_past_4gib_refused(codec, dev):
     st = torch.empty(100, dtype=torch.int32, device=dev)
     L = hd.lib()
     rv = L.nghttp2_amd_hd_huff_decode_batch_auto(
-        hd._p(src), hd._p(so), 100, hd._p(dst), (1 << 32) + 64, hd._p(doff), hd._p(st), None,
-        None, hd._stream(None))
+        hd._p(src), hd._p(so), 100, int(off[-1]), hd._p(dst), (1 << 32) + 64, hd._p(doff),
+        hd._p(st), None, None, hd._stream(None))
     assert rv == hd.NGHTTP2_ERR_INVALID_ARGUMENT
 
 
