@@ -23,7 +23,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <cassert>
 #include <deque>
 #include <unordered_map>
 #include <mutex>
@@ -564,18 +563,20 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     std::vector<size_t> ref_max(conns.size());
     for (size_t c = 0; c < conns.size(); ++c)
       ref_max[c] = std::max<size_t>({64u, conns[c]->settings_max, conns[c]->bufsize_max});
+    // (saturating: a table limit near SIZE_MAX must not wrap the bound)
+    auto sat = [](uint64_t a, uint64_t b) -> uint64_t { return a > UINT64_MAX - b ? UINT64_MAX : a + b; };
     uint64_t nv_bound = 0, ar_bound = 0;
     auto lit_len = [&](const Lit &l) -> uint64_t {
       if (l.huff < 0) return l.len;
       return hst[l.huff] >= 0 ? (uint64_t)hst[l.huff] : (uint64_t)l.len * 8u / 5u + 1u;
     };
     for (uint32_t i = 0; i < nblocks && !may_cut; ++i) {
-      const uint64_t rm = ref_max[conn_of[inflaters[i]]];
+      const uint64_t rm = std::min<uint64_t>(ref_max[conn_of[inflaters[i]]], UINT32_MAX);
       for (const Op &op : bl[i].ops) {
         if (op.kind == Op::SIZE) continue;
         ++nv_bound;
-        if (op.kind == Op::INDEXED) ar_bound += rm + 2u;
-        else ar_bound += (op.new_name ? lit_len(op.name) : rm) + lit_len(op.val) + 2u;
+        if (op.kind == Op::INDEXED) ar_bound = sat(ar_bound, rm + 2u);
+        else ar_bound = sat(ar_bound, sat(sat(op.new_name ? lit_len(op.name) : rm, lit_len(op.val)), 2u));
       }
       may_cut = nv_bound > nva_cap || ar_bound > arena_cap;
     }
@@ -602,8 +603,17 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       break;
     }
   }
+  if (cut < nblocks && !may_cut) {
+    // the bound missed an output that fits no cap: the tables are past the
+    // cut with no snapshot to restore, so the batch fails and its inflaters
+    // turn bad (an internal error, never expected)
+    for (auto *c : conns) c->bad = true;
+    for (uint32_t j = 0; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_FATAL;
+    *nva_used = 0;
+    *arena_used = 0;
+    return NGHTTP2_AMD_ERR_FATAL;
+  }
   if (cut < nblocks) {  // restore, then re-apply the blocks before the cut
-    assert(may_cut);  // the bound covers every output that fits no cap
     for (size_t c = 0; c < conns.size(); ++c) *conns[c] = std::move(snap[c]);
     BlockOut scratch;
     for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, scratch);

@@ -17,7 +17,8 @@ import pytest
 from oracle import hpack_oracle as HO
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(REPO, "nghttp2_amd", "bin")
+# NGHTTP2_AMD_BIN: another build of the drivers (tests/test_sanitize.py: the ASan one)
+BIN = os.environ.get("NGHTTP2_AMD_BIN") or os.path.join(REPO, "nghttp2_amd", "bin")
 GOLD = os.path.join(REPO, "tests", "golden")
 
 
