@@ -138,11 +138,14 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, cons
  *                 :823-863, RFC 7541 5.1);
  *   payload       the Huffman bytes (nghttp2_hd_huff_encode) or the raw ones.
  * The literals are back to back in string order, ready to be spliced into
- * header blocks in wire order.
+ * header blocks in wire order.  Two launches: the encode count (code bits
+ * per string, tile sums of the literal lengths) and the encode pack, which
+ * writes every literal -- prefix and payload -- straight into dst (no
+ * intermediate Huffman pool).
  *
  *   raw_bytes : src_off[n] - src_off[0] (sizes the bounds below)
  *   dst_cap   : >= nghttp2_amd_hd_emit_strings_bound(raw_bytes, n)
- *   workspace : device scratch, 256-byte aligned,
+ *   workspace : device scratch (the tile sums),
  *               >= nghttp2_amd_hd_emit_strings_workspace_size(raw_bytes, n)
  */
 NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_emit_strings_bound(uint64_t raw_bytes, uint32_t n);

@@ -2,8 +2,9 @@
  * nghttp2_amd_hd_testing.h -- test hooks of the batched HPACK front-ends.
  *
  * Not part of the drop-in boundary: the parity tests use these to force the
- * code paths a small test batch would not take on its own.  Both are
- * process-wide settings read at the next nghttp2_amd_hd_deflate_blocks call.
+ * code paths a small test batch would not take on its own (the two switches
+ * are process-wide settings read at the next nghttp2_amd_hd_deflate_blocks
+ * call), and the bench its copy ceiling.
  */
 #ifndef NGHTTP2_AMD_HD_TESTING_H
 #define NGHTTP2_AMD_HD_TESTING_H
@@ -25,6 +26,13 @@ NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__test_fail_deflate_gpu(int n);
 /* Batches of at least n header names take the GPU name-token kernel (the
  * default threshold keeps small batches on the host). */
 NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__set_gpu_names_min(uint32_t n);
+
+/* Device-to-device streaming copy of `bytes` bytes (16-byte aligned, a
+ * multiple of 64) on `stream`: four 16-byte loads in flight per lane over a
+ * grid-stride loop.  bench.py times it as the measured HBM ceiling that the
+ * roofline's frac_vs_copy is taken against. */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__copy_calib(void *dst, const void *src, size_t bytes,
+                                                  void *stream);
 
 #ifdef __cplusplus
 }

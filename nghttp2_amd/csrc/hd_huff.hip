@@ -30,7 +30,10 @@
 //                   kept as the exact cross-check path and for chunked calls
 //   k_slot_len / k_scan_tiles / k_scan_apply   tight decode slots
 //                   (floor(8E/5)+1 each)
-//   k_frame_len / k_frame_copy   HPACK string literals (emit_string)
+//   k_enc_count<true> / k_encode<true>   HPACK string literals (emit_string,
+//                   lib/nghttp2_hd.c:1001-1044) packed straight into wire
+//                   order: prefix (H bit, 7-bit-prefix length) + Huffman or
+//                   raw payload
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -38,6 +41,7 @@
 #include <type_traits>
 
 #include "../../include/nghttp2_amd_hd.h"
+#include "../../include/nghttp2_amd_hd_testing.h"
 
 namespace dev {
 #define HD_TBL static __device__
@@ -256,6 +260,22 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 
 #define ENC_WAVES 4                  // waves per encode workgroup (tile = 256 strings)
 
+// bytes of the 7-bit-prefix integer n (count_encoded_length(n, 7))
+__device__ __forceinline__ uint32_t prefix7_len(uint32_t n) {
+  if (n < 127u) return 1u;
+  n -= 127u;
+  uint32_t len = 2u;
+  for (; n >= 128u; n >>= 7) ++len;
+  return len;
+}
+// byte r of the literal's prefix (encode_length(buf, n, 7) with buf[0] = H)
+__device__ __forceinline__ uint32_t prefix7_byte(uint32_t n, uint32_t h, uint32_t r) {
+  if (r == 0) return (h << 7) | (n < 127u ? n : 127u);
+  const uint32_t m = (n - 127u) >> (7u * (r - 1u));
+  return (m & 0x7Fu) | (m >= 128u ? 0x80u : 0u);
+}
+
+
 // ---------------------------------------------------------------------------
 // encode over aligned chunks (the product path): a wave owns 64 consecutive
 // strings, i.e. the contiguous raw bytes [A, Z), and walks them as aligned
@@ -269,6 +289,9 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 // (in-chunk exclusive prefixes to LDS, 16 bits a byte), a wave scan places
 // the chunks, and every string lane reads P at its two ends.  Bytes before
 // A or past Z in the edge chunks add the same amount to both ends.
+// FR (emit_string, lib/nghttp2_hd.c:1001-1044): the tile sums are of the
+// string LITERALS' bytes, prefix7_len(P) + P with P = min(E, R) (H = E < R).
+template <bool FR>
 __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
                                                   const uint32_t *__restrict__ off,
                                                   uint32_t n,
@@ -342,6 +365,10 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     const uint32_t bits = sl ? Pb - Pa : 0u;
     e = (bits + 7u) >> 3;
     if (sl && out_len) out_len[t0 + lane] = bits_out ? bits : e;
+    if (FR && sl) {
+      const uint32_t R = b_l - a_l, P = e < R ? e : R;
+      e = prefix7_len(P) + P;
+    }
   }
   if (tile_sums) {
     uint32_t tot;
@@ -367,6 +394,8 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
 #define EC_M 16u                    // image margin (words): >= 15 bytes x 30 bits
 #define EC_RW (EC_M + 1024u + 32u)  // + 1 KB at <= 32 bits a byte + carry + bytes past Z
+// FR: + the wave's literal prefixes and pads (64 x (6 x 8 + 7) bits)
+#define EC_RW_F (EC_RW + 112u)
 
 // OR the MSB-aligned bits {hi, lo} into the image at bit b
 __device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, uint32_t lo) {
@@ -377,31 +406,54 @@ __device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, ui
   atomicOr((uint32_t *)&q[2], __builtin_amdgcn_alignbit(lo, 0u, o));  // (0 when o = 0)
 }
 
+// FR: emit_string (lib/nghttp2_hd.c:1001-1044) fused into the pack -- every
+// string leaves as its HPACK string literal, back to back in wire order:
+// the prefix (H bit, 7-bit-prefix length of P = min(E, R), :823-863) and the
+// Huffman payload (H = E < R) or the raw bytes.  In the wave's bit stream a
+// literal's prefix bits are extra length attached to the input byte before
+// the string (the previous string's last byte; at the wave start, an initial
+// offset), so the stream stays the concatenation of the bytes' codes (raw
+// strings: the byte itself, 8 bits) and the extra bits; the prefix values
+// and the pads' ones are OR'ed in by the string's own lane.  Extras reach
+// tens of bits, so FR combines codes in 64-bit pairs (not 32-bit pairs and
+// quads) and keeps the per-byte extras as u16.
+template <bool FR>
 __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
                                                const uint32_t *__restrict__ tile_sums) {
+  constexpr uint32_t RW = FR ? EC_RW_F : EC_RW;
+  constexpr uint32_t PDW = FR ? 512u : 256u;  // u16 extras / u8 pads per round byte
   __shared__ uint2 codeT[256];  // {code MSB-aligned, length}
-  __shared__ uint32_t image[ENC_WAVES][EC_RW];
-  __shared__ alignas(16) uint32_t padb[ENC_WAVES][256];  // a round's pad bits (u8 per byte)
+  __shared__ uint32_t image[ENC_WAVES][RW];
+  __shared__ alignas(16) uint32_t padb[ENC_WAVES][PDW];  // a round's pad bits (u8 per byte)
+  __shared__ uint32_t rawm[ENC_WAVES][FR ? 32 : 1];       // FR: a round's raw-string bytes
   __shared__ uint32_t o_sh[WG + 1];
   __shared__ uint32_t red[2 * (WG / 64)];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
   lds_u32 *img = (lds_u32 *)image[wv];
-  for (uint32_t i = lane; i < EC_RW; i += 64u) img[i] = 0u;
+  for (uint32_t i = lane; i < RW; i += 64u) img[i] = 0u;
   lds_u32 *pdw = (lds_u32 *)padb[wv];
   lds_u8 *pdb = (lds_u8 *)padb[wv];
+  lds_u16 *pdh = (lds_u16 *)padb[wv];
+  lds_u32 *rwm = (lds_u32 *)rawm[wv];
 #pragma unroll
-  for (uint32_t i = 0; i < 4u; ++i) pdw[lane + 64u * i] = 0u;
+  for (uint32_t i = 0; i < PDW / 64u; ++i) pdw[lane + 64u * i] = 0u;
   const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
   const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
-  const uint32_t E_me = (bits_me + 7u) >> 3;
   const uint32_t t0 = blockIdx.x * WG + 64u * wv;
   const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
   const bool sl = lane < nstr;
   const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+  // (thread s_me is lane `lane` of string t0 + lane)
+  const uint32_t Eh_me = (bits_me + 7u) >> 3;  // Huffman bytes
+  const uint32_t R_me = b_l - a_l;
+  const bool H_me = FR && Eh_me < R_me;        // FR: the literal is Huffman-coded
+  const uint32_t P_me = FR ? (H_me ? Eh_me : R_me) : 0u;
+  const uint32_t PL_me = FR && sl ? prefix7_len(P_me) : 0u;
+  const uint32_t E_me = FR ? (sl ? PL_me + P_me : 0u) : Eh_me;  // output bytes of string s_me
   const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
   const uint32_t Z = nstr ? __builtin_amdgcn_readlane(b_l, nstr - 1u) : 0u;
   const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
@@ -448,17 +500,48 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   if (nstr == 0) return;
   const uint32_t OA = o_sh[64u * wv], OZ = o_sh[64u * wv + nstr];  // the wave's output bytes
   const uint64_t G0 = 8ull * OA;
-  const uint32_t pad_l = sl ? 8u * E_me - bits_me : 0u;  // EOS-prefix bits after string l
+  const uint32_t pad_l = sl && (!FR || H_me) ? 8u * Eh_me - bits_me : 0u;  // EOS-prefix bits after string l
   const uint32_t olast_l = o_me + E_me - 1u;             // its last output byte (if E > 0)
   const uint32_t tail_l = b_l - 1u;                      // its last raw byte
+  // FR: the prefixes of the strings that start at the wave's first byte go
+  // before it (an initial offset XS); every other string's prefix is extra
+  // length of the byte before it; raw strings (any in the wave: anyraw) take
+  // their bytes as 8-bit codes
+  const bool at_a = FR && sl && a_l == A;
+  const uint32_t XS = FR ? __builtin_amdgcn_readlane(wave_incl_scan(at_a ? 8u * PL_me : 0u), 63) : 0u;
+  const bool rawl = FR && sl && !H_me && R_me > 0u;
+  const bool anyraw = FR && __ballot(rawl) != 0;
+  // (FR: a wave of empty strings only still has its literals: one round)
+  const uint32_t c_stop = FR && c_end == c0 ? c0 + 1u : c_end;
   uint32_t x = 0;  // output bit of the round's first wave byte (relative to G0)
-  for (uint32_t cb = c0; cb < c_end; cb += 64u) {
-    const bool first = cb == c0, last_round = cb + 64u >= c_end;
+  for (uint32_t cb = c0; cb < c_stop; cb += 64u) {
+    const bool first = cb == c0, last_round = cb + 64u >= c_stop;
     const uint32_t base = cb << 4;
     const uint64_t WB = (G0 + x) >> 5;  // global word of img[EC_M]
     // ---- pads of the strings ending in this round, at their last raw byte
     const bool tl = sl && pad_l && b_l > a_l && tail_l - base < 1024u;
-    if (tl) pdb[tail_l - base] = (uint8_t)pad_l;
+    // FR: my prefix as extra length of the byte before my string
+    const bool pfx = FR && sl && a_l > A && a_l - 1u - base < 1024u;
+    if (!FR) {
+      if (tl) pdb[tail_l - base] = (uint8_t)pad_l;
+    } else {
+      if (tl) atomicAdd((uint32_t *)&pdw[(tail_l - base) >> 1], pad_l << (16u * ((tail_l - base) & 1u)));
+      if (pfx) atomicAdd((uint32_t *)&pdw[(a_l - 1u - base) >> 1], (8u * PL_me) << (16u * ((a_l - 1u - base) & 1u)));
+      if (anyraw) {
+        if (lane < 32u) rwm[lane] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t lo = max(a_l, base), hi = min(b_l, base + 1024u);
+        if (rawl && lo < hi) {
+          for (uint32_t w = (lo - base) >> 5; w <= (hi - 1u - base) >> 5; ++w) {
+            const uint32_t w0 = base + 32u * w;
+            const uint32_t f = max(lo, w0) - w0, t = min(hi, w0 + 32u) - w0;  // bits [f, t)
+            atomicOr((uint32_t *)&rwm[w], (t - f == 32u ? 0xFFFFFFFFu : ((1u << (t - f)) - 1u)) << f);
+          }
+        }
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -467,34 +550,74 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
     wn = make_uint4(0, 0, 0, 0);
     if (cb + 64u + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + p0 + 1024u);
-    const u32x4 pdv = *(const lds_u32x4 *)(pdw + 4u * lane);
-    const uint32_t pd[4] = {pdv.x, pdv.y, pdv.z, pdv.w};
 #define EC_B8(j) (((j) & 3) ? (wd[(j) >> 2] >> (8 * ((j) & 3) - 3)) & 0x7F8u : (wd[(j) >> 2] << 3) & 0x7F8u)
-    // per input dword: four codes (+ the pad at a string's last byte) ->
-    // two pairs {pc, pl} (MSB-aligned, < 32 bits) -> one quad {qh:qo, ql}
-    uint32_t qh[4], qo[4], ql[4], plx = 0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      uint32_t c[4], l[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(4 * m + u));
-        c[u] = cj.x;
-        l[u] = cj.y + ((pd[m] >> (8 * u)) & 0xFFu);
+    // (!FR) per input dword: four codes (+ the pad at a string's last byte)
+    // -> two pairs {pc, pl} (MSB-aligned, < 32 bits) -> one quad {qh:qo, ql};
+    // (FR) per byte pair: {ph:po} (MSB-aligned, <= 64 bits), length pq
+    uint32_t pd[FR ? 8 : 4];
+    {
+      const u32x4 pdv = *(const lds_u32x4 *)(pdw + (FR ? 8u : 4u) * lane);
+      pd[0] = pdv.x; pd[1] = pdv.y; pd[2] = pdv.z; pd[3] = pdv.w;
+      if (FR) {
+        const u32x4 pdv2 = *(const lds_u32x4 *)(pdw + 8u * lane + 4u);
+        pd[4 % (FR ? 8 : 4)] = pdv2.x; pd[5 % (FR ? 8 : 4)] = pdv2.y;
+        pd[6 % (FR ? 8 : 4)] = pdv2.z; pd[7 % (FR ? 8 : 4)] = pdv2.w;
       }
-      const uint32_t pl0 = l[0] + l[1], pl1 = l[2] + l[3];
-      const uint32_t pc0 = c[0] | (c[1] >> l[0]), pc1 = c[2] | (c[3] >> l[2]);
-      plx = max(plx, max(pl0, pl1));
-      ql[m] = pl0 + pl1;
-      qh[m] = pc0 | (pc1 >> pl0);
-      qo[m] = __builtin_amdgcn_alignbit(pc1, 0u, pl0);
     }
-    const uint32_t S = act ? ql[0] + ql[1] + ql[2] + ql[3] : 0u;
-    const bool longp = __ballot(act && plx > 31u) != 0;  // a pair of 32 bits or more: bytewise
+    const uint32_t rm = FR && anyraw ? (rwm[lane >> 1] >> (16u * (lane & 1u))) & 0xFFFFu : 0u;
+    // (FR) the first chunk's bytes before A take no bits: the wave-start
+    // prefixes (XS) are the first bits of the image, stored
+    const uint32_t km = FR && first && lane == 0u ? (1u << (A & 15u)) - 1u : 0u;
+    uint32_t qh[FR ? 8 : 4], qo[FR ? 8 : 4], ql[FR ? 8 : 4], plx = 0;
+    if (!FR) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint32_t c[4], l[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(4 * m + u));
+          c[u] = cj.x;
+          l[u] = cj.y + ((pd[m] >> (8 * u)) & 0xFFu);
+        }
+        const uint32_t pl0 = l[0] + l[1], pl1 = l[2] + l[3];
+        const uint32_t pc0 = c[0] | (c[1] >> l[0]), pc1 = c[2] | (c[3] >> l[2]);
+        plx = max(plx, max(pl0, pl1));
+        ql[m] = pl0 + pl1;
+        qh[m] = pc0 | (pc1 >> pl0);
+        qo[m] = __builtin_amdgcn_alignbit(pc1, 0u, pl0);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t c[2], l[2], xt[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int j = 2 * k + u;
+          const uint32_t b8 = EC_B8(j);
+          const uint2 cj = *(const uint2 *)((const char *)codeT + b8);
+          const bool raw = (rm >> j) & 1u, skip = (km >> j) & 1u;
+          c[u] = skip ? 0u : raw ? b8 << 21 : cj.x;  // a raw byte: itself, MSB-aligned
+          l[u] = skip ? 0u : raw ? 8u : cj.y;
+          xt[u] = (pd[k % (FR ? 8 : 4)] >> (16 * u)) & 0xFFFFu;
+        }
+        const uint32_t L0 = l[0] + xt[0];  // c1 starts L0 bits after c0
+        const uint64_t v = ((uint64_t)c[1] << 32) >> (L0 & 63u);
+        plx = max(plx, L0 + l[1]);
+        qh[k % (FR ? 8 : 4)] = c[0] | (uint32_t)(v >> 32);
+        qo[k % (FR ? 8 : 4)] = (uint32_t)v;
+        ql[k % (FR ? 8 : 4)] = L0 + l[1] + xt[1];
+      }
+    }
+    uint32_t S = 0;
+#pragma unroll
+    for (int m = 0; m < (FR ? 8 : 4); ++m) S += ql[m];
+    S = act ? S : 0u;
+    // a pair of 32 (FR: 64) bits or more: bytewise
+    const bool longp = __ballot(act && plx > (FR ? 64u : 31u)) != 0;
     // ---- the first chunk's bytes before A go before the wave's first bit
     // (no pads there)
     uint32_t RA = 0;
-    if (first) {
+    if (!FR && first) {
       const uint32_t k = A & 15u;
       uint32_t ra = 0;
 #pragma unroll
@@ -503,13 +626,14 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
       RA = __builtin_amdgcn_readfirstlane(ra);
     }
     const uint32_t Sinc = wave_incl_scan(S);
+    const uint32_t X0 = first ? XS : 0u;  // (FR) the wave-start prefixes
     // my chunk's first bit in the image (img[0] = global word WB - EC_M)
-    const uint32_t ib0 = (uint32_t)(G0 + x - 32ull * WB) + 32u * EC_M + (Sinc - S) - RA;
+    const uint32_t ib0 = (uint32_t)(G0 + x - 32ull * WB) + 32u * EC_M + (Sinc - S) + X0 - RA;
     if (act) {
       if (!longp) {
         uint32_t b = ib0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < (FR ? 8 : 4); ++m) {
           ec_or3(img, b, qh[m], qo[m]);
           b += ql[m];
         }
@@ -518,13 +642,24 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
 #pragma unroll 1
         for (uint32_t m = 0; m < 4u; ++m) {
           const uint32_t w = m == 0 ? wd[0] : m == 1 ? wd[1] : m == 2 ? wd[2] : wd[3];
-          const uint32_t pw = m == 0 ? pd[0] : m == 1 ? pd[1] : m == 2 ? pd[2] : pd[3];
+          const uint32_t pw = m == 0 ? pd[0] : m == 1 ? pd[1] : m == 2 ? pd[2] : pd[3 % (FR ? 8 : 4)];
+          const uint32_t pw2 = FR ? (m == 0 ? pd[1] : m == 1 ? pd[3] : m == 2 ? pd[5 % (FR ? 8 : 4)]
+                                                                          : pd[7 % (FR ? 8 : 4)]) : 0u;
+          const uint32_t pwf = FR ? (m == 0 ? pd[0] : m == 1 ? pd[2] : m == 2 ? pd[4 % (FR ? 8 : 4)]
+                                                                          : pd[6 % (FR ? 8 : 4)]) : pw;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint32_t b8 = u ? (w >> (8 * u - 3)) & 0x7F8u : (w << 3) & 0x7F8u;
             const uint2 cj = *(const uint2 *)((const char *)codeT + b8);
-            ec_or3(img, b, cj.x, 0u);
-            b += cj.y + ((pw >> (8 * u)) & 0xFFu);
+            if (FR) {
+              const bool raw = (rm >> (4u * m + u)) & 1u, skip = (km >> (4u * m + u)) & 1u;
+              const uint32_t xw = u < 2 ? pwf : pw2;
+              ec_or3(img, b, skip ? 0u : raw ? b8 << 21 : cj.x, 0u);
+              b += (skip ? 0u : raw ? 8u : cj.y) + ((xw >> (16 * (u & 1))) & 0xFFFFu);
+            } else {
+              ec_or3(img, b, cj.x, 0u);
+              b += cj.y + ((pw >> (8 * u)) & 0xFFu);
+            }
           }
         }
       }
@@ -535,11 +670,21 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
       const uint32_t r = (uint32_t)((olast_l >> 2) - WB) + EC_M;
       atomicOr((uint32_t *)&img[r], ((1u << pad_l) - 1u) << (24u - 8u * (olast_l & 3u)));
     }
+    // ---- (FR) the literal prefixes attached in this round: H bit and the
+    // 7-bit-prefix length (encode_length, lib/nghttp2_hd.c:823-863) at the
+    // literal's first output bytes
+    if (FR && (pfx || (first && at_a))) {
+      for (uint32_t r = 0; r < PL_me; ++r) {
+        const uint32_t q = o_me + r;
+        const uint32_t v = prefix7_byte(P_me, H_me ? 1u : 0u, r);
+        atomicOr((uint32_t *)&img[(uint32_t)((q >> 2) - WB) + EC_M], v << (24u - 8u * (q & 3u)));
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- store whole words and zero them; carry a partial last word
-    const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) - RA;
+    const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) + X0 - RA;
     const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
     const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
     // words [ilo, ihi) lie inside the wave's output [OA, OZ) (<= dst_cap by
@@ -561,7 +706,12 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
       }
     }
     if (first && lane < EC_M) img[lane] = 0u;  // the bytes before A
-    if (tl) pdb[tail_l - base] = 0u;
+    if (!FR) {
+      if (tl) pdb[tail_l - base] = 0u;
+    } else {
+      if (tl) pdh[tail_l - base] = 0u;
+      if (pfx) pdh[a_l - 1u - base] = 0u;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1868,112 +2018,20 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
   }
 }
 
-// ---------------------------------------------------------------------------
-// HPACK string literals: emit_string (lib/nghttp2_hd.c:1001-1044), batched
-// ---------------------------------------------------------------------------
-// A literal is the H bit (0x80 iff the Huffman form is strictly shorter,
-// :1011) with the payload length as a 7-bit-prefix integer
-// (count_encoded_length / encode_length, :823-863), then the payload: the
-// Huffman bytes or the raw ones.  After a batch encode into the workspace,
-// k_frame_len sizes each literal, a tile scan places them, and k_frame_copy
-// writes the output stream dword by dword (coalesced stores), gathering each
-// byte from the prefix, the Huffman pool or the raw pool.
-
-// bytes of the 7-bit-prefix integer n (count_encoded_length(n, 7))
-__device__ __forceinline__ uint32_t prefix7_len(uint32_t n) {
-  if (n < 127u) return 1u;
-  n -= 127u;
-  uint32_t len = 2u;
-  for (; n >= 128u; n >>= 7) ++len;
-  return len;
-}
-// byte r of the literal's prefix (encode_length(buf, n, 7) with buf[0] = H)
-__device__ __forceinline__ uint32_t prefix7_byte(uint32_t n, uint32_t h, uint32_t r) {
-  if (r == 0) return (h << 7) | (n < 127u ? n : 127u);
-  const uint32_t m = (n - 127u) >> (7u * (r - 1u));
-  return (m & 0x7Fu) | (m >= 128u ? 0x80u : 0u);
-}
-
-// out_len[s] = literal bytes of string s; tile sums for the offset scan.
-__global__ __launch_bounds__(WG) void k_frame_len(const uint32_t *__restrict__ src_off,
-                                                  const uint32_t *__restrict__ enc_off, uint32_t n,
-                                                  uint32_t *__restrict__ out_len,
-                                                  uint32_t *__restrict__ tile_sums) {
-  __shared__ uint32_t red[WG / 64];
-  const uint32_t s = blockIdx.x * WG + threadIdx.x;
-  uint32_t f = 0;
-  if (s < n) {
-    const uint32_t R = src_off[s + 1] - src_off[s], E = enc_off[s + 1] - enc_off[s];
-    const uint32_t P = E < R ? E : R;
-    f = prefix7_len(P) + P;
-    out_len[s] = f;
+// the measured HBM ceiling (nghttp2_amd_hd__copy_calib): a grid-stride
+// copy, four 16-byte loads in flight per lane
+__global__ __launch_bounds__(WG) void k_copy_calib(uint4 *__restrict__ dst,
+                                                   const uint4 *__restrict__ src, uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * WG;
+  uint64_t i = (uint64_t)blockIdx.x * WG + threadIdx.x;
+  for (; i + 3u * stride < n16; i += 4u * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2u * stride], d = src[i + 3u * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2u * stride] = c;
+    dst[i + 3u * stride] = d;
   }
-  uint32_t tot;
-  block_excl_scan<WG>(f, red, &tot);
-  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
-}
-
-// One workgroup per tile of 256 literals: the tile's output bytes
-// [dst_off[t0], dst_off[t0 + 256]) go out as dwords, one per thread and
-// pass; a dword shared with a neighbouring tile goes bytewise.
-__global__ __launch_bounds__(WG) void k_frame_copy(const uint8_t *__restrict__ src,
-                                                   const uint32_t *__restrict__ src_off,
-                                                   const uint8_t *__restrict__ enc,
-                                                   const uint32_t *__restrict__ enc_off, uint32_t n,
-                                                   uint8_t *__restrict__ dst, uint64_t dst_cap,
-                                                   const uint32_t *__restrict__ dst_off) {
-  __shared__ uint32_t fo[WG + 1];   // literal starts (tile-relative to nothing: absolute)
-  __shared__ uint32_t pay[WG];      // payload length | H << 31
-  __shared__ uint32_t psrc[WG];     // payload source offset (enc or src pool)
-  __shared__ uint8_t plen[WG];
-  const uint32_t t0 = blockIdx.x * WG;
-  const uint32_t nt = min(n - t0, (uint32_t)WG);
-  const uint32_t s = t0 + threadIdx.x;
-  if (threadIdx.x < nt) {
-    const uint32_t a = src_off[s], R = src_off[s + 1] - a;
-    const uint32_t e = enc_off[s], E = enc_off[s + 1] - e;
-    const bool h = E < R;
-    const uint32_t P = h ? E : R;
-    fo[threadIdx.x] = dst_off[s];
-    pay[threadIdx.x] = P | (h ? 0x80000000u : 0u);
-    psrc[threadIdx.x] = h ? e : a;
-    plen[threadIdx.x] = (uint8_t)prefix7_len(P);
-  }
-  if (threadIdx.x == 0) fo[nt] = dst_off[t0 + nt];
-  __syncthreads();
-  const uint32_t lo = fo[0], hi = fo[nt];
-  if (hi == lo) return;
-  for (uint32_t w = (lo >> 2) + threadIdx.x; w <= ((hi - 1u) >> 2); w += WG) {
-    const uint32_t p0 = 4u * w;
-    // the literal holding the first in-range byte of this dword
-    const uint32_t pf = max(p0, lo);
-    uint32_t a = 0, b = nt - 1u;
-    while (a < b) {  // last i with fo[i] <= pf
-      const uint32_t m = (a + b + 1u) >> 1;
-      if (fo[m] <= pf) a = m; else b = m - 1u;
-    }
-    uint32_t i = a, v = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4u; ++j) {
-      const uint32_t p = p0 + j;
-      if (p < lo || p >= hi) continue;
-      while (p >= fo[i + 1]) ++i;  // empty literals do not exist: each has >= 1 byte
-      const uint32_t r = p - fo[i], L = plen[i], P = pay[i] & 0x7FFFFFFFu;
-      const bool h = pay[i] >> 31;
-      uint32_t byte;
-      if (r < L) byte = prefix7_byte(P, h ? 1u : 0u, r);
-      else byte = (h ? enc : src)[psrc[i] + (r - L)];
-      v |= byte << (8u * j);
-    }
-    if (p0 >= lo && p0 + 4u <= hi && p0 + 4u <= dst_cap) {
-      *reinterpret_cast<uint32_t *>(dst + p0) = v;
-    } else {
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t p = p0 + j;
-        if (p >= lo && p < hi && p < dst_cap) dst[p] = (uint8_t)(v >> (8u * j));
-      }
-    }
-  }
+  for (; i < n16; i += stride) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -2086,7 +2144,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
                                            uint32_t n, uint32_t *enc_len, void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_enc_count, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
+  hipLaunchKernelGGL(k_enc_count<false>, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
                      src_off, n, enc_len, (uint32_t *)nullptr, 0);
   return hip_rv(hipGetLastError());
 }
@@ -2103,8 +2161,8 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
-  hipLaunchKernelGGL(k_encode, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
+  hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_encode<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
 }
@@ -2115,13 +2173,16 @@ size_t nghttp2_amd_hd_emit_strings_bound(uint64_t raw_bytes, uint32_t n) {
   return (size_t)((b + 15u) & ~(uint64_t)15u);
 }
 
-// workspace: [tile scratch][encoded offsets (n + 1)][encoded pool]
-static size_t a256(size_t x) { return (x + 255u) & ~(size_t)255u; }
+// workspace: the tile sums of the literal lengths
 size_t nghttp2_amd_hd_emit_strings_workspace_size(uint64_t raw_bytes, uint32_t n) {
-  return a256(nghttp2_amd_hd_huff_workspace_size(n)) + a256(4u * ((size_t)n + 1u)) +
-         a256(nghttp2_amd_hd_huff_encode_bound(raw_bytes, n));
+  (void)raw_bytes;
+  return nghttp2_amd_hd_huff_workspace_size(n);
 }
 
+// emit_string for a batch in two launches: k_enc_count<true> (code bits per
+// string, tile sums of the literal lengths) and k_encode<true> (literal
+// offsets, then every literal -- prefix and Huffman or raw payload --
+// packed straight into the wire stream)
 int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_off, uint32_t n,
                                       uint64_t raw_bytes, uint8_t *dst, size_t dst_cap,
                                       uint32_t *dst_off, void *workspace, size_t workspace_size,
@@ -2130,25 +2191,23 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
   if (!dst_off) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if (n == 0) return hip_rv(hipMemsetAsync(dst_off, 0, sizeof(uint32_t), st));
   if (!src || !src_off || !dst || !workspace) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if (((uintptr_t)workspace & 255u) ||
-      workspace_size < nghttp2_amd_hd_emit_strings_workspace_size(raw_bytes, n) ||
+  if (workspace_size < nghttp2_amd_hd_emit_strings_workspace_size(raw_bytes, n) ||
       dst_cap < nghttp2_amd_hd_emit_strings_bound(raw_bytes, n))
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  uint8_t *w = (uint8_t *)workspace;
-  uint32_t *tiles = (uint32_t *)w;
-  const size_t ws_t = a256(nghttp2_amd_hd_huff_workspace_size(n));
-  uint32_t *eoff = (uint32_t *)(w + ws_t);
-  uint8_t *epool = w + ws_t + a256(4u * ((size_t)n + 1u));
-  const size_t ecap = nghttp2_amd_hd_huff_encode_bound(raw_bytes, n);
-  int rv = nghttp2_amd_hd_huff_encode_batch(src, src_off, n, epool, ecap, eoff, tiles, ws_t, stream);
-  if (rv) return rv;
   const uint32_t nt = ntiles_for(n);
-  hipLaunchKernelGGL(k_frame_len, dim3(nt), dim3(WG), 0, st, src_off, (const uint32_t *)eoff, n,
-                     dst_off, tiles);
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(SCAN_WG), 0, st, tiles, nt, dst_off + n);
-  hipLaunchKernelGGL(k_scan_apply, dim3(nt), dim3(WG), 0, st, dst_off, n, (const uint32_t *)tiles);
-  hipLaunchKernelGGL(k_frame_copy, dim3(nt), dim3(WG), 0, st, src, src_off, (const uint8_t *)epool,
-                     (const uint32_t *)eoff, n, dst, (uint64_t)dst_cap, (const uint32_t *)dst_off);
+  uint32_t *tiles = (uint32_t *)workspace;
+  hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_encode<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+  return hip_rv(hipGetLastError());
+}
+
+int nghttp2_amd_hd__copy_calib(void *dst, const void *src, size_t bytes, void *stream) {
+  if (!dst || !src || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u) || (bytes & 63u))
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (bytes == 0) return 0;
+  hipLaunchKernelGGL(k_copy_calib, dim3(NUM_CU * 8), dim3(WG), 0, (hipStream_t)stream, (uint4 *)dst,
+                     (const uint4 *)src, (uint64_t)(bytes / 16u));
   return hip_rv(hipGetLastError());
 }
 

@@ -225,9 +225,7 @@ class HuffmanBatchCodec:
         if dst_off is None:
             dst_off = self._empty(n + 1, torch.int32, stream)
         need = self.L.nghttp2_amd_hd_emit_strings_workspace_size(int(raw_bytes), n)
-        ews = self._scratch_for("ews", need + 256, stream)
-        base = (256 - ews.data_ptr() % 256) % 256  # (the API wants it 256-byte aligned)
-        ews = ews[base:base + need]
+        ews = self._scratch_for("ews", need, stream)
         rv = self.L.nghttp2_amd_hd_emit_strings_batch(
             _p(src), _p(src_off), n, int(raw_bytes), _p(dst), dst.numel(), _p(dst_off),
             _p(ews), ews.numel(), _stream(stream))
