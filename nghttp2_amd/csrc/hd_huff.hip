@@ -306,10 +306,12 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
   __syncthreads();
   const uint32_t t0 = blockIdx.x * WG + 64u * wv;  // the wave's strings
   uint32_t e = 0;
+  bool huge = false;
   if (t0 < n) {
     const uint32_t nstr = min(n - t0, 64u);
     const bool sl = lane < nstr;
     const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+    huge = b_l - a_l > NGHTTP2_AMD_ENCODE_MAX_STRING;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
     const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
@@ -371,9 +373,12 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     }
   }
   if (tile_sums) {
-    uint32_t tot;
-    block_excl_scan<WG>(e, red, &tot);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+    uint32_t tot, nhuge;
+    // a string whose code bits would not fit the 32-bit counts poisons its
+    // tile's sum (0xFFFFFFFF), so this tile and every one after it overflow
+    // in k_encode
+    block_excl_scan_sum<WG>(e, huge ? 1u : 0u, red, &tot, &nhuge);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = nhuge ? 0xFFFFFFFFu : tot;
   }
 }
 
@@ -474,10 +479,13 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
 #pragma unroll
     for (int k = 0; k < 8; ++k) pre += p8[k];
   }
-  uint32_t tot, ptot_lo, ptot_hi;
+  uint32_t tot32, ptot_lo, ptot_hi;
   // the 64-bit prefix as two 32-bit sums: 256 parts of 23 bits fit 31 bits
-  const uint32_t loc = block_excl_scan_sum<WG>(E_me, (uint32_t)(pre & 0x7FFFFFu), red, &tot,
+  const uint32_t loc = block_excl_scan_sum<WG>(E_me, (uint32_t)(pre & 0x7FFFFFu), red, &tot32,
                                                &ptot_lo);  // (barriers)
+  // (a string too long for the 32-bit code-bit counts poisoned the tile's
+  // sum: the tile overflows)
+  const uint64_t tot = tile_sums[blockIdx.x] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
   {
     uint32_t dummy;
     block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);

@@ -214,6 +214,32 @@ def test_encode_total_past_4gib_marks_overflow(codec, dev):
     torch.cuda.empty_cache()
 
 
+def test_encode_string_past_max_marks_overflow(codec, dev):
+    """A string of more than NGHTTP2_AMD_ENCODE_MAX_STRING raw bytes (its code
+    bits would pass the kernels' 32-bit counts) marks the batch overflowed,
+    even when the encoded total would fit the pool (as the header says); the
+    tiles before it are exact."""
+    import torch
+    max_string = 0xFFFFFFFF // 30
+    L0 = 600
+    n_small = 300  # two tiles of 256 strings before ... the long one lies in the second
+    huge = max_string + 1
+    lens = [L0] * n_small + [huge]
+    off = np.zeros(len(lens) + 1, dtype=np.int64)
+    off[1:] = np.cumsum(lens)
+    raw = int(off[-1])
+    src = torch.full((raw + 32,), ord("a"), dtype=torch.uint8, device=dev)
+    enc, eoff = codec.encode(src, to_dev(off.astype(np.uint32), dev), raw_bytes=raw)
+    torch.cuda.synchronize()
+    eo = _u32(eoff)
+    assert eo[-1] == 0xFFFFFFFF, "overflow mark"
+    one, _ = O.encode_batch(np.full(L0 + 16, ord("a"), np.uint8), np.array([0, L0], np.uint32))
+    E1 = len(one)
+    assert np.array_equal(eo[:257].astype(np.int64), np.arange(257) * E1), "first tile exact"
+    del enc, src
+    torch.cuda.empty_cache()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

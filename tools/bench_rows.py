@@ -25,14 +25,19 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def bench_emit(steps=20):
+def bench_emit(steps=20, cfg=2):
+    """emit_strings on the config-2 (pseudo-headers) or config-3 (mixed
+    values) batch: wall time per batch, and the launch pair's time by HIP
+    events on its stream; roofline bytes R + F + 12 N (raw in, literals out,
+    offsets) per batch against 8 TB/s."""
     import torch
     import nghttp2_amd
     from nghttp2_amd import workloads as W
     from oracle import oracle as O
     dev = torch.device("cuda:0")
-    pool, off = W.gen_pseudo_headers(1 << 20)
+    pool, off = W.gen_pseudo_headers(1 << 20) if cfg == 2 else W.gen_mixed_values(1 << 20)
     raw = int(off[-1])
+    n = len(off) - 1
     codec = nghttp2_amd.HuffmanBatchCodec(dev)
     src = torch.from_numpy(pool).to(dev)
     so = torch.from_numpy(off.view(np.int32)).to(dev)
@@ -51,9 +56,23 @@ def bench_emit(steps=20):
         codec.emit_strings(src, so, raw_bytes=raw, dst=dst, dst_off=do)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / steps
+    s = torch.cuda.current_stream()
+    ev = []
+    for _ in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        codec.emit_strings(src, so, raw_bytes=raw, dst=dst, dst_off=do)
+        b.record(s)
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    tk = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3
     F = int(do[-1].item())
-    return {"strings": len(off) - 1, "raw_bytes": raw, "literal_bytes": F,
-            "ms_per_batch": round(t * 1e3, 4), "GBps_raw_plus_out": round((raw + F) / t / 1e9, 1)}
+    alg = raw + F + 12 * n
+    return {"config": cfg, "strings": n, "raw_bytes": raw, "literal_bytes": F,
+            "ms_per_batch": round(t * 1e3, 4), "GBps_raw_plus_out": round((raw + F) / t / 1e9, 1),
+            "roofline": {"kernels": "k_enc_count<true> + k_encode<true>", "launch_pair_ms": round(tk * 1e3, 4),
+                         "alg_bytes": alg, "achieved_GBps": round(alg / tk / 1e9, 1),
+                         "frac_of_8TBps": round(alg / tk / 8e12, 4)}}
 
 
 def bench_names(steps=50, long_frac=0.02):
@@ -140,7 +159,8 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
 
 
 if __name__ == "__main__":
-    rows = sys.argv[1:] or ["emit", "inflate", "names"]
-    fns = {"emit": bench_emit, "inflate": bench_inflate, "names": bench_names,
+    rows = sys.argv[1:] or ["emit", "emit3", "inflate", "names"]
+    fns = {"emit": bench_emit, "emit3": lambda: bench_emit(cfg=3), "inflate": bench_inflate,
+           "names": bench_names,
            "names_short": lambda: bench_names(long_frac=0.0)}
     print(json.dumps({r: fns[r]() for r in rows}, indent=1))
