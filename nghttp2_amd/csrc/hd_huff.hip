@@ -259,6 +259,9 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 }
 
 #define ENC_WAVES 4                  // waves per encode workgroup (tile = 256 strings)
+#ifndef EC_CNT_PFD
+#define EC_CNT_PFD 2  // k_enc_count: rounds of chunks in flight per wave
+#endif
 
 // bytes of the 7-bit-prefix integer n (count_encoded_length(n, 7))
 __device__ __forceinline__ uint32_t prefix7_len(uint32_t n) {
@@ -319,16 +322,21 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     const lds_u16 *pr16 = (const lds_u16 *)pre[wv];
     uint32_t Rc = 0, Pa = 0, Pb = 0;
     bool ga = false, gb = false;
-    // chunks are loaded two rounds ahead (enough bytes in flight per CU)
-    uint4 wn = make_uint4(0, 0, 0, 0), wn2 = make_uint4(0, 0, 0, 0);
-    if (c0 + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + ((c0 + lane) << 4));
-    if (c0 + 64u + lane < c_end) wn2 = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u + lane) << 4));
+    // chunks are loaded EC_CNT_PFD rounds ahead
+    uint4 q[EC_CNT_PFD];
+#pragma unroll
+    for (uint32_t d = 0; d < EC_CNT_PFD; ++d) {
+      q[d] = make_uint4(0, 0, 0, 0);
+      if (c0 + 64u * d + lane < c_end) q[d] = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u * d + lane) << 4));
+    }
     for (uint32_t cb = c0; cb < c_end; cb += 64u) {
       const uint32_t base = cb << 4;
-      const uint32_t wd[4] = {wn.x, wn.y, wn.z, wn.w};
-      wn = wn2;
-      wn2 = make_uint4(0, 0, 0, 0);
-      if (cb + 128u + lane < c_end) wn2 = *reinterpret_cast<const uint4 *>(src + base + 2048u + 16u * lane);
+      const uint32_t wd[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
+#pragma unroll
+      for (uint32_t d = 0; d + 1 < EC_CNT_PFD; ++d) q[d] = q[d + 1];
+      q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
+      if (cb + 64u * EC_CNT_PFD + lane < c_end)
+        q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
       uint32_t run = 0, pk[8];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -2026,20 +2034,25 @@ __global__ __launch_bounds__(WG) void k_decode_fsm(const uint8_t *__restrict__ s
   }
 }
 
-// the measured HBM ceiling (nghttp2_amd_hd__copy_calib): a grid-stride
-// copy, four 16-byte loads in flight per lane
+// the measured HBM ceiling (nghttp2_amd_hd__copy_calib): each workgroup
+// copies contiguous 16 KB blocks (four coalesced 16-byte loads in flight
+// per lane, nontemporal), the grid striding over the blocks
 __global__ __launch_bounds__(WG) void k_copy_calib(uint4 *__restrict__ dst,
                                                    const uint4 *__restrict__ src, uint64_t n16) {
-  const uint64_t stride = (uint64_t)gridDim.x * WG;
-  uint64_t i = (uint64_t)blockIdx.x * WG + threadIdx.x;
-  for (; i + 3u * stride < n16; i += 4u * stride) {
-    const uint4 a = src[i], b = src[i + stride], c = src[i + 2u * stride], d = src[i + 3u * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2u * stride] = c;
-    dst[i + 3u * stride] = d;
+  const uint64_t nblk = n16 / (4u * WG);
+  for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const uint64_t i = b * 4u * WG + threadIdx.x;
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(s4 + i + k * WG);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], d4 + i + k * WG);
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+  for (uint64_t i = nblk * 4u * WG + (uint64_t)blockIdx.x * WG + threadIdx.x; i < n16;
+       i += (uint64_t)gridDim.x * WG)
+    dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------

@@ -33,7 +33,8 @@ def main():
     out_path = os.path.join(ROOT, "profiles", "traffic.json")
     res = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for cfg, strings in ((2, 1 << 20), (3, 1 << 20), (5, 1 << 20)):
-        d = os.path.join(ROOT, "gpurun_out", "pmc_c%d" % cfg)
+        base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
+        d = os.path.join(base, "pmc_c%d" % cfg)
         if not os.path.isdir(d):
             continue
         fetch = per_launch(os.path.join(d, "p1"), "FETCH_SIZE")
@@ -44,9 +45,9 @@ def main():
                 rd, wr = 2.0 * fetch[k] * 1024, write[k] * 1024
                 ent[k] = {"strings": strings, "read_bytes": int(rd), "write_bytes": int(wr),
                           "hbm_bytes_per_launch": int(rd + wr),
-                          "source": "gpurun_out/pmc_c%d (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
-                                    "FETCH x2 per MI355X_MICROARCH.md)" % cfg}
-        res["config%d" % cfg] = ent
+                          "source": "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                                    "FETCH x2 per MI355X_MICROARCH.md)" % os.path.relpath(d, ROOT)}
+        res.setdefault("config%d" % cfg, {}).update(ent)
     json.dump(res, open(out_path, "w"), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
 
