@@ -292,24 +292,28 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 // A or past Z in the edge chunks add the same amount to both ends.
 // FR (emit_string, lib/nghttp2_hd.c:1001-1044): the tile sums are of the
 // string LITERALS' bytes, prefix7_len(P) + P with P = min(E, R) (H = E < R).
+// k_enc_count: strings per wave (a tile of 256 is 256 / SPW waves); 32 / 16
+// measured slower (config 3 encode pair 137.5 / 146.3 vs 135.8 us)
+#define EC_CNT_SPW 64u
+#define EC_CNT_NT (WG * 64u / EC_CNT_SPW)
 template <bool FR>
-__global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restrict__ src,
                                                   const uint32_t *__restrict__ off,
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
                                                   uint32_t *__restrict__ tile_sums,
                                                   int bits_out) {
   __shared__ uint8_t lenT[256];
-  __shared__ alignas(16) uint32_t pre[ENC_WAVES][512];  // a round's prefixes (u16 per byte)
-  __shared__ uint32_t red[WG / 64];
+  __shared__ alignas(16) uint32_t pre[EC_CNT_NT / 64][512];  // a round's prefixes (u16 per byte)
+  __shared__ uint32_t red[2 * EC_CNT_NT / 64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+  if (threadIdx.x < 256) lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
   __syncthreads();
-  const uint32_t t0 = blockIdx.x * WG + 64u * wv;  // the wave's strings
+  const uint32_t t0 = blockIdx.x * WG + EC_CNT_SPW * wv;  // the wave's strings
   uint32_t e = 0;
   bool huge = false;
   if (t0 < n) {
-    const uint32_t nstr = min(n - t0, 64u);
+    const uint32_t nstr = min(n - t0, EC_CNT_SPW);
     const bool sl = lane < nstr;
     const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
     huge = b_l - a_l > NGHTTP2_AMD_ENCODE_MAX_STRING;
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(WG) void k_enc_count(const uint8_t *__restrict__ sr
     // a string whose code bits would not fit the 32-bit counts poisons its
     // tile's sum (0xFFFFFFFF), so this tile and every one after it overflow
     // in k_encode
-    block_excl_scan_sum<WG>(e, huge ? 1u : 0u, red, &tot, &nhuge);
+    block_excl_scan_sum<EC_CNT_NT>(e, huge ? 1u : 0u, red, &tot, &nhuge);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = nhuge ? 0xFFFFFFFFu : tot;
   }
 }
@@ -2186,7 +2190,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
                                            uint32_t n, uint32_t *enc_len, void *stream) {
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  hipLaunchKernelGGL(k_enc_count<false>, dim3(ntiles_for(n)), dim3(WG), 0, (hipStream_t)stream, src,
+  hipLaunchKernelGGL(k_enc_count<false>, dim3(ntiles_for(n)), dim3(EC_CNT_NT), 0, (hipStream_t)stream, src,
                      src_off, n, enc_len, (uint32_t *)nullptr, 0);
   return hip_rv(hipGetLastError());
 }
@@ -2203,7 +2207,7 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
   hipLaunchKernelGGL(k_encode<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
@@ -2238,7 +2242,7 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
   hipLaunchKernelGGL(k_encode<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
                      (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
