@@ -1445,25 +1445,28 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       DD_REFILL();                                                       \
     }                                                                    \
   } while (0)
-  while ((int32_t)bp <= G2) {
-    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
-    const uint32_t U1 = E_USED(e1);
-    bb <<= U1;
-    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];
-    sink.put2(e1, e2);
-    const uint32_t U2 = E_USED(e2);
-    if (SYNC) {
-      pb = bp;
-      le1 = e1;
-      le2 = e2;
-      ls = 0;
-    }
-    bb <<= U2;
-    bp += U1 + U2;
-    nb -= U1 + U2;
-    DD_REFILL();
-    if (e2 == 0u) DD_SLOW();  // (an e1 of 0 stalls e2 too)
-  }
+#define DD_PAIR()                                                        \
+  do {                                                                   \
+    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];  \
+    const uint32_t U1 = E_USED(e1);                                      \
+    bb <<= U1;                                                           \
+    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];  \
+    sink.put2(e1, e2);                                                   \
+    const uint32_t U2 = E_USED(e2);                                      \
+    if (SYNC) {                                                          \
+      pb = bp;                                                           \
+      le1 = e1;                                                          \
+      le2 = e2;                                                          \
+      ls = 0;                                                            \
+    }                                                                    \
+    bb <<= U2;                                                           \
+    bp += U1 + U2;                                                       \
+    nb -= U1 + U2;                                                       \
+    DD_REFILL();                                                         \
+    if (e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */            \
+  } while (0)
+  while ((int32_t)bp <= G2) DD_PAIR();
+#undef DD_PAIR
 #undef DD_SLOW
   if (SYNC && !failed && (int32_t)bp >= (int32_t)bstop) {
     // the last pair passed bstop: its codeword boundaries in order are the
