@@ -1376,24 +1376,29 @@ struct DDRun {
 // Decode from bp (advanced in place) to the first codeword boundary >=
 // bstop, or to the string end bend (tail analysis), into sink.
 //
-// Fast steps come from a register bit buffer: bb holds the stream's bits
-// [bp, 32 k) MSB first (nb of them, >= 32 at a step's start), refilled
-// without a branch from the staged dword k (prefetched in nxt), so a step's
-// only dependent memory access is its lookup.  A fast step needs its 14
-// lookup bits inside the string (bp + 14 <= bend) and must not pass the
-// first boundary >= bstop (bp <= bstop - 13: the first symbol of a 2-symbol
-// entry is <= 9 bits); pairs run while both steps qualify.  A code longer
-// than the lookup (entry 0) stalls the lane for the rest of the pair, then
-// goes through slow_entry; one that would pass the string end is its tail
-// and leaves the fast loop.  The last bits go through checked steps (LDS
-// windows), which also settle the tail: the undecoded t < 30 bits.
-#define DD_REFILL()                                                      \
+// Steps read a register window: A is the staged word holding bit bp - 1, B
+// the next, N the one after (prefetched); with nq = ~(bp - 1) the 32 stream
+// bits from bp are alignbit(A, B, nq), so a step's only dependent memory
+// access is its lookup.  A step or pair advances < 32 bits: at most one word
+// boundary, two selects (DD_ADV).  (Round 3: the 64-bit bit buffer this
+// replaces, shifted per step and refilled by compare and 64-bit shift, took
+// ~6 VALU more per pair: config 3 decode 301.3 vs 295.0 us.)  A fast step
+// needs its 14 lookup bits inside the string (bp + 14 <= bend) and must not
+// pass the first boundary >= bstop (bp <= bstop - 13: the first symbol of a
+// 2-symbol entry is <= 9 bits); pairs run while both steps qualify.  A code
+// longer than the lookup (entry 0) stalls the lane for the rest of the pair,
+// then goes through slow_entry; one that would pass the string end is its
+// tail and leaves the fast loop.  The last bits go through checked steps,
+// which also settle the tail: the undecoded t < 30 bits.
+#define DD_ADV(U)                                                        \
   do {                                                                   \
-    const bool t_ = nb < 32u;                                            \
-    bb |= (uint64_t)(t_ ? nxt : 0u) << ((32u - nb) & 63u);               \
-    nb += t_ ? 32u : 0u;                                                 \
-    k += t_ ? 1u : 0u;                                                   \
-    nxt = ib(k);                                                         \
+    const uint32_t n2_ = nq - (U);                                       \
+    const bool t_ = ((n2_ ^ nq) >> 5) != 0u;                             \
+    nq = n2_;                                                            \
+    A = t_ ? B : A;                                                      \
+    B = t_ ? N : B;                                                      \
+    kw += t_ ? 1 : 0;                                                    \
+    N = ib((uint32_t)kw + 2u);                                           \
   } while (0)
 // PAIRS: only the fast pairs, none starting past `lim` (no careful steps):
 // bp stops at a codeword boundary on the way, for a caller that records it
@@ -1416,70 +1421,65 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // overshoot for the items' own decode measured slower: 314.5 vs 303.6 us)
   int32_t G2 = min((int32_t)bstop - (SYNC ? 1 : 2 * TT::BITS - 4), (int32_t)bend - 2 * TT::BITS);
   if (PAIRS) G2 = min(G2, lim);
-  uint32_t pb = bp, le1 = 0, le2 = 0, ls = 0;  // (SYNC) the last pair: start, entries, slow code
-  uint32_t k = bp >> 5;
-  const uint32_t o = bp & 31u;
-  const uint32_t w0 = ib(k), w1 = ib(k + 1u);
-  uint64_t bb = (((uint64_t)w0 << 32) | w1) << o;
-  uint32_t nb = 64u - o;
-  k += 2u;
-  uint32_t nxt = ib(k);
-  // a code longer than the lookup inside the pair loop (nb >= 32): decode
-  // it, or leave the pair loop at EOS (failed) or at the string's tail
-  // (the careful steps find it again)
+  // (SYNC) the last pair: start (as nq), entries, slow code
+  uint32_t pb = ~(bp - 1u), le1 = 0, le2 = 0, ls = 0;
+  // (bp = 0: A is the dword before the staged words, never inside a window)
+  int32_t kw = (int32_t)(bp - 1u) >> 5;
+  uint32_t A = ib((uint32_t)kw), B = ib((uint32_t)kw + 1u), N = ib((uint32_t)kw + 2u);
+  uint32_t nq = ~(bp - 1u);
+  int32_t nG = ~(G2 - 1);  // bp <= G2  <=>  (int) nq >= ~(G2 - 1)
+  // the window words in before the loop (else the loop head waits for every
+  // LDS access in flight, the prefetch of N included, each pair)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  // a code longer than the lookup inside the pair loop: decode it, or leave
+  // the pair loop at EOS (failed) or at the string's tail (the careful steps
+  // find it again)
 #define DD_SLOW()                                                        \
   do {                                                                   \
-    const uint32_t rem_ = bend - bp;                                     \
-    const uint32_t e_ = slow_entry(T, (uint32_t)(bb >> 32), rem_);       \
+    const uint32_t rem_ = bend - (~nq + 1u);                             \
+    const uint32_t e_ = slow_entry(T, __builtin_amdgcn_alignbit(A, B, nq), rem_); \
     if (e_ == 0xFFFFFFFFu) {                                             \
       failed = true;                                                     \
-      G2 = INT32_MIN;                                                    \
+      nG = INT32_MAX;                                                    \
     } else if (E_L1(e_) > rem_) {                                        \
-      G2 = INT32_MIN;                                                    \
+      nG = INT32_MAX;                                                    \
     } else {                                                             \
       sink.put(e_ & 0xFFFFu, E_CNT8(e_));                                \
       const uint32_t U_ = E_USED(e_);                                    \
       if (SYNC) ls = U_;                                                 \
-      bb <<= U_;                                                         \
-      bp += U_;                                                          \
-      nb -= U_;                                                          \
-      DD_REFILL();                                                       \
+      DD_ADV(U_);                                                        \
     }                                                                    \
-  } while (0)
-#define DD_PAIR()                                                        \
-  do {                                                                   \
-    const uint32_t e1 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];  \
-    const uint32_t U1 = E_USED(e1);                                      \
-    bb <<= U1;                                                           \
-    const uint32_t e2 = T.lut[(uint32_t)(bb >> 32) >> (32 - TT::BITS)];  \
-    sink.put2(e1, e2);                                                   \
-    const uint32_t U2 = E_USED(e2);                                      \
-    if (SYNC) {                                                          \
-      pb = bp;                                                           \
-      le1 = e1;                                                          \
-      le2 = e2;                                                          \
-      ls = 0;                                                            \
-    }                                                                    \
-    bb <<= U2;                                                           \
-    bp += U1 + U2;                                                       \
-    nb -= U1 + U2;                                                       \
-    DD_REFILL();                                                         \
-    if (e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */            \
   } while (0)
   // The fast pairs run at raised wave priority: the SIMD issues their
   // dependent chain's VALU before other waves' staging, scans and stores
   // (config 3 decode 294.1 vs 297.7 us, config 2 50.6 vs 52.2; priority 3,
   // or priority over the whole run with its careful steps: no better)
   __builtin_amdgcn_s_setprio(1);
-  while ((int32_t)bp <= G2) DD_PAIR();
+  while ((int32_t)nq >= nG) {
+    const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
+    const uint32_t e1 = T.lut[w >> (32 - TT::BITS)];
+    const uint32_t U1 = E_USED(e1);
+    const uint32_t e2 = T.lut[(w << U1) >> (32 - TT::BITS)];
+    sink.put2(e1, e2);
+    const uint32_t U2 = E_USED(e2);
+    if (SYNC) {
+      pb = nq;  // (as bp after the loop)
+      le1 = e1;
+      le2 = e2;
+      ls = 0;
+    }
+    DD_ADV(U1 + U2);
+    if (e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */
+  }
   __builtin_amdgcn_s_setprio(0);
-#undef DD_PAIR
 #undef DD_SLOW
+  bp = ~nq + 1u;
   if (SYNC && !failed && (int32_t)bp >= (int32_t)bstop) {
     // the last pair passed bstop: its codeword boundaries in order are the
     // ends of e1's first symbol and of e1, of e2's first symbol and of e2
     // (or of the long code decoded after e1); the entry is the first one at
     // or after bstop (a 1-symbol entry's first end is its end)
+    pb = ~pb + 1u;
     const uint32_t c1 = pb + (le1 ? E_L1(le1) : ls), c2 = pb + E_USED(le1);
     const uint32_t c3 = c2 + (le2 ? E_L1(le2) : ls), c4 = c2 + (le2 ? E_USED(le2) : ls);
     bp = c1 >= bstop ? c1 : c2 >= bstop ? c2 : c3 >= bstop ? c3 : c4;
@@ -1499,7 +1499,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     bool done = failed || (int32_t)bp >= (int32_t)bstop;
     while (__ballot(!done)) {
       if (!done) {
-        const uint32_t w = (uint32_t)(bb >> 32);
+        const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
         uint32_t e = T.lut[w >> (32 - TT::BITS)];
         if (e == 0u) e = slow_entry(T, w, 30u);
         const uint32_t L1 = E_L1(e), adv = bp + L1 >= bstop ? L1 : E_USED(e);
@@ -1507,10 +1507,8 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
           failed = true;
           done = true;
         } else {
-          bb <<= adv;
           bp += adv;
-          nb -= adv;
-          DD_REFILL();
+          DD_ADV(adv);
           done = bp >= bstop;
         }
       }
@@ -1528,7 +1526,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   bool done = failed;
   {
     while (__ballot(!done)) {
-      const uint32_t w = (uint32_t)(bb >> 32);
+      const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
       const uint32_t rem = bend - bp;
       const bool stop = done || bp >= bstop || rem == 0u;
       uint32_t e = T.lut[w >> (32 - TT::BITS)];
@@ -1547,9 +1545,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
       sink.put(take2 ? (e & 0xFFFFu) : (take1 ? (e & 0xFFu) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
       bp += adv;
-      bb <<= adv;
-      nb -= adv;
-      DD_REFILL();
+      DD_ADV(adv);
       failed = failed || eos;
       done = done || eos || !take1 || bp >= bstop;
     }
@@ -1559,7 +1555,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   r.failed = failed;
   return r;
 }
-#undef DD_REFILL
+#undef DD_ADV
 
 // Status and final decode context of a string (lib/nghttp2_hd_huffman.c:
 // 135-142) from its tail: as finish_string, with the FSM state (three table
