@@ -176,6 +176,7 @@ struct ByteOut {
 // Address-space-explicit pointers, so LDS staging compiles to ds_* and
 // global output to global_* (never flat_*).
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
@@ -289,7 +290,6 @@ __device__ __forceinline__ uint32_t prefix7_byte(uint32_t n, uint32_t h, uint32_
 // strings, i.e. the contiguous raw bytes [A, Z), and walks them as aligned
 // 16-byte chunks, 64 per round (one per lane), whatever the string lengths.
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
 // Pass 1 (lib/nghttp2_hd_huffman.c:34-43): code bits per string.  With P(x)
 // = the code bits of the wave's bytes from its first chunk up to byte x, a
@@ -1339,6 +1339,9 @@ struct LdsPtrSink {
   __device__ __forceinline__ LdsPtrSink(lds_u8 *b) : p(b), base(b) {}
   __device__ __forceinline__ uint32_t count() const { return (uint32_t)(p - base); }
   __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    // (round 3: one ds_write_b16 at the byte address -- the LDS runs in
+    // unaligned mode, tools/diag/probe -- measured slower: 354.9 vs 296.2 us
+    // on config 3, the hardware splits misaligned stores)
     p[0] = (uint8_t)v;
     p[1] = (uint8_t)(v >> 8);
     p += c8 >> 3;
@@ -1392,9 +1395,9 @@ struct DDRun {
 // which also settle the tail: the undecoded t < 30 bits.
 #define DD_ADV(U)                                                        \
   do {                                                                   \
-    const uint32_t n2_ = nq - (U);                                       \
-    const bool t_ = ((n2_ ^ nq) >> 5) != 0u;                             \
-    nq = n2_;                                                            \
+    const uint32_t u_ = (U);                                             \
+    const bool t_ = u_ > (nq & 31u); /* (bp - 1) & 31 = 31 - (nq & 31) */ \
+    nq -= u_;                                                            \
     A = t_ ? B : A;                                                      \
     B = t_ ? N : B;                                                      \
     kw += t_ ? 1 : 0;                                                    \

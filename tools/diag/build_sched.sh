@@ -6,7 +6,7 @@ set -e
 HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../../nghttp2_amd/csrc/hd_huff.hip
 F="-O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=gfx950"
-rm -f $HERE/lib_*.so
+[ -n "${KEEP:-}" ] || rm -f $HERE/lib_*.so  # KEEP=1: add to the libraries there
 O=$(mktemp -d)
 PART=${PART:-DEC}
 if [ "$PART" = DEC ]; then FIXED="-DHD_PART_ENC"; VAR=DEC
