@@ -771,12 +771,17 @@ enum {  // code lengths longer than the lookup (14-bit primary set, 13-bit set)
 
 #define NLONG_PAD 16  // search width (padding rows repeat the last row)
 static_assert(NLONG <= NLONG_PAD && NLONG13 <= NLONG_PAD, "long-code search too narrow");
-// Lookup entry (tools/gen_tables.py): sym1 | sym2 << 8 | 8 cnt << 16 | L1 << 21 | used << 27
-// (sym2 = 0 when cnt = 1: the low half is the entry's output bytes as they stand)
-#define E_CNT8(e) (((e) >> 16) & 0x18u)
-#define E_CNT(e) (((e) >> 19) & 3u)
-#define E_L1(e) (((e) >> 21) & 31u)
+// Lookup entry (tools/gen_tables.py): sym1 | L1 << 8 | cnt << 13 | sym2 << 16 | used << 27
+// (sym2 = 0 when cnt = 1).  The output bytes are bits 0..7 and 16..23 (E_OUT2):
+// the item decoder stores the second with ds_write_b8_d16_hi, no shift (round
+// 3; sym2 in bits 8..15 took a shift per entry).  A sink's put/put_nf take
+// their bytes in that form.
+#define E_CNT8(e) (((e) >> 10) & 0x18u)
+#define E_CNT(e) (((e) >> 13) & 3u)
+#define E_L1(e) (((e) >> 8) & 31u)
 #define E_USED(e) ((e) >> 27)
+#define E_OUT2 0x00FF00FFu
+#define E_OUT1 0x000000FFu
 // The decoder's LDS tables for an LB-bit first-level lookup (14: 64 KB, the
 // most two-symbol entries; 13: 32 KB, which leaves room for more waves).
 template <int LB>
@@ -908,7 +913,8 @@ struct CheckedDwordSink {
   }
   __device__ __forceinline__ uint32_t count() const { return n8 >> 3; }
   __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
-    acc |= (uint64_t)v << nb;
+    // the entry's bytes 0 and 2 as a contiguous pair (byte 1, 3: zero)
+    acc |= (uint64_t)__builtin_amdgcn_perm(0u, v, 0x0C0C0200u) << nb;
     nb += c8;
     n8 += c8;
   }
@@ -953,7 +959,7 @@ __device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32
   const uint32_t L = T.long_len[i];
   const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
   if (L <= rem && sym == 256) return 0xFFFFFFFFu;
-  return (L <= rem ? sym : 0u) | (8u << 16) | (L << 21) | (L << 27);
+  return (L <= rem ? sym : 0u) | (L << 8) | (1u << 13) | (L << 27);
 }
 
 // First-level miss: the second level (codes of up to 16 bits), else the search.
@@ -1016,7 +1022,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
         e = 0u;                                                  \
       }                                                          \
     }                                                            \
-    sink.put_nf(e & 0xFFFFu, E_CNT8(e));                         \
+    sink.put_nf(e & E_OUT2, E_CNT8(e));                          \
     q += E_USED(e);                                              \
   } while (0)
   while ((int32_t)q < F2) {
@@ -1052,7 +1058,7 @@ __device__ __forceinline__ SubOut decode_item(const DecTables &T, const lds_u32 
       break;
     }
     const bool two = E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
-    sink.put(two ? e & 0xFFFFu : e & 0xFFu, two ? 16u : 8u);
+    sink.put(two ? e & E_OUT2 : e & E_OUT1, two ? 16u : 8u);
     bp += two ? U : L1;
   }
   if (!failed && bp == bend) r.at_end = true;
@@ -1343,12 +1349,12 @@ struct LdsPtrSink {
     // unaligned mode, tools/diag/probe -- measured slower: 354.9 vs 296.2 us
     // on config 3, the hardware splits misaligned stores)
     p[0] = (uint8_t)v;
-    p[1] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)(v >> 16);
     p += c8 >> 3;
   }
   __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
-    put_nf(e1 & 0xFFFFu, E_CNT8(e1));
-    put_nf(e2 & 0xFFFFu, E_CNT8(e2));
+    put_nf(e1, E_CNT8(e1));  // (byte stores: no mask)
+    put_nf(e2, E_CNT8(e2));
   }
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
   __device__ __forceinline__ void flush() {}
@@ -1447,7 +1453,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     } else if (E_L1(e_) > rem_) {                                        \
       nG = INT32_MAX;                                                    \
     } else {                                                             \
-      sink.put(e_ & 0xFFFFu, E_CNT8(e_));                                \
+      sink.put(e_ & E_OUT2, E_CNT8(e_));                                 \
       const uint32_t U_ = E_USED(e_);                                    \
       if (SYNC) ls = U_;                                                 \
       DD_ADV(U_);                                                        \
@@ -1546,7 +1552,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       r.t = tail ? rem : r.t;
       r.win = tail ? w : r.win;
       const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
-      sink.put(take2 ? (e & 0xFFFFu) : (take1 ? (e & 0xFFu) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
+      sink.put(take2 ? (e & E_OUT2) : (take1 ? (e & E_OUT1) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
       bp += adv;
       DD_ADV(adv);
       failed = failed || eos;

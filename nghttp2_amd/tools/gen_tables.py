@@ -167,11 +167,12 @@ def build():
     # LUT_BITS-bit multi-symbol lookup table for the canonical decoder: for
     # every window, the first code if it is <= LUT_BITS bits (sym1, L1) and,
     # when the rest of the window holds another whole code, the second (sym2).
-    # Entry: sym1 | sym2 << 8 | 8 cnt << 16 | L1 << 21 | used << 27, with
+    # Entry: sym1 | L1 << 8 | cnt << 13 | sym2 << 16 | used << 27, with
     # cnt = symbols in the entry (1 or 2), used = bits they take, and sym2 = 0
-    # when cnt = 1, so that the low half is the entry's output bytes as they
-    # stand and bits 16..20 the output bits.  A zero entry means the first code is longer than LUT_BITS (all
-    # such codes start with >= 10 ones).
+    # when cnt = 1: the output bytes are bits 0..7 and 16..23 (a decoder
+    # stores the second with no shift, ds_write_b8_d16_hi), and (e >> 10) &
+    # 0x18 the output bits.  A zero entry means the first code is longer than
+    # LUT_BITS (all such codes start with >= 10 ones).
     lut = []
     for w in range(1 << LUT_BITS):
         def first_code(v, nbits):
@@ -186,14 +187,14 @@ def build():
             assert s1 != EOS
             r = LUT_BITS - L1
             s2, L2 = first_code(w & ((1 << r) - 1), r) if r else (None, 0)
-            e = s1 | (8 << 16) | (L1 << 21) | (L1 << 27)
+            e = s1 | (L1 << 8) | (1 << 13) | (L1 << 27)
             if s2 is not None:
                 assert L1 + L2 <= LUT_BITS < 32
-                e = s1 | (s2 << 8) | (16 << 16) | (L1 << 21) | ((L1 + L2) << 27)
+                e = s1 | (L1 << 8) | (2 << 13) | (s2 << 16) | ((L1 + L2) << 27)
         lut.append(e)
     # second level for codes of LUT_BITS+1..16 bits: every code longer than 12
     # bits starts with 10 ones; indexed by the 6 window bits after them.  Entry
-    # as above with cnt 1 (sym | 8 << 16 | L << 21 | L << 27); 0 = longer code.
+    # as above with cnt 1 (sym | L << 8 | 1 << 13 | L << 27); 0 = longer code.
     lut2 = []
     for v in range(64):
         w16 = (0x3FF << 6) | v
@@ -202,7 +203,7 @@ def build():
             sym = leaf.get((w16 >> (16 - L), L))
             if sym is not None:
                 assert sym != EOS
-                e = sym | (8 << 16) | (L << 21) | (L << 27)
+                e = sym | (L << 8) | (1 << 13) | (L << 27)
                 break
         lut2.append(e)
     for code, L in enc:
@@ -274,7 +275,7 @@ def write_inc(t, path):
     for i in range(0, 256, 16):
         w("  " + ", ".join("%d" % v for v in t["id_list"][i:i + 16]) + ",")
     w("};")
-    w("/* canonical decoder: %d-bit lookup, sym1 | sym2 << 8 | 8 cnt << 16 | L1 << 21 | used << 27 */" % LUT_BITS)
+    w("/* canonical decoder: %d-bit lookup, sym1 | L1 << 8 | cnt << 13 | sym2 << 16 | used << 27 */" % LUT_BITS)
     w("#define HD_HUFF_LUT_BITS %d" % LUT_BITS)
     w("HD_TBL const unsigned int hd_huff_lut[%d] = {" % (1 << LUT_BITS))
     for i in range(0, 1 << LUT_BITS, 8):
