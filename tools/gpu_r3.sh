@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 record on one GPU box: parity suite, smoke, bench (configs 3 + 2,
-# 5), kernel-trace stats (one stream), FETCH/WRITE PMC passes (configs 2, 3),
+# 5, host-resident), kernel-trace stats (one stream), FETCH/WRITE PMC passes (configs 2, 3),
 # the 8(f) rows (emit, inflate, names) with their kernel stats.  Every GPU
 # step has its own limit; a failing step ends the script.
 set -u
@@ -14,12 +14,13 @@ run() {
   echo "== $name rc=$rc"; tail -n 2 "$O/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
 }
-for s in ${STEPS:-pytest smoke bench bench5 prof pmc rows}; do
+for s in ${STEPS:-pytest smoke bench bench5 host prof pmc rows}; do
   case $s in
     pytest) run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     bench5) run bench5 600 python bench.py --config 5 ;;
+    host)   run bench_host 600 python bench.py --host-resident --no-cpu-baseline ;;
     prof)   rm -rf $O/prof3s1 $O/prof2s1
             run prof3s1 300 rocprofv3 --kernel-trace --stats -d $O/prof3s1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --streams 1 --config 3
             run prof2s1 300 rocprofv3 --kernel-trace --stats -d $O/prof2s1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1 --config 2 ;;
