@@ -480,6 +480,49 @@ def auto_decode_check(codec, dev, enc, eoff, tag, pick=None, nthreads=1):
     return st, do
 
 
+def window_edge_batch():
+    """Encoded strings aimed at the item decoder's register window (round 3):
+    30-bit codes and 5-bit codes at every bit alignment inside and across
+    pieces, strings of whole 32-bit words, and invalid encodings (EOS inside a
+    pair, all-ones tails, random bytes) that fail at varied bit positions."""
+    rng = np.random.default_rng(31)
+    long_syms = [10, 13, 22]  # 30-bit codes (RFC 7541 Appendix B)
+    strs = []
+    for shift in range(64):
+        strs.append(b"0" * shift + bytes([10]) + b"a" * (shift % 7))
+        strs.append(bytes([13]) * (1 + shift % 5) + b"0" * shift)
+        strs.append(b"e" * shift + bytes(rng.choice(long_syms, 3).astype(np.uint8)) + b"t" * (63 - shift))
+    for k in range(40):
+        body = bytearray(rng.choice(np.frombuffer(b"0123456789aceiost", np.uint8), 300 + 17 * k))
+        for p in rng.integers(0, len(body), 1 + k % 6):
+            body[int(p)] = int(rng.choice(long_syms))
+        strs.append(bytes(body))
+    for w in range(1, 40):
+        strs.append(b"0" * (32 * w))  # 160 w bits: ends on a word boundary, no padding
+    strs.append(b"")
+    off = np.zeros(len(strs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(x) for x in strs])
+    pool = np.frombuffer(b"".join(strs), dtype=np.uint8).copy()
+    enc, eoff = O.encode_batch(pool, off)
+    bad = [b"\xff" * k for k in range(1, 12)]  # EOS after 30 bits, or a bad tail
+    for k in range(60):  # a valid prefix, then EOS at a varied bit position
+        v = bytes(enc[int(eoff[k]):int(eoff[k + 1])])
+        bad.append(v[: len(v) // 2] + b"\xff\xff\xff\xfc" + v[len(v) // 2:])
+    bad += [bytes(rng.integers(0, 256, int(rng.integers(1, 200)), dtype=np.uint8)) for _ in range(60)]
+    enc2 = np.concatenate([enc[:int(eoff[-1])], np.frombuffer(b"".join(bad), dtype=np.uint8)])
+    eoff2 = np.concatenate([eoff, int(eoff[-1]) + np.cumsum([len(x) for x in bad]).astype(np.uint32)])
+    return enc2, eoff2.astype(np.uint32)
+
+
+@pytest.mark.parametrize("pick", ["items64", "pieces40"])
+def test_decode_auto_window_edges(codec, dev, pick):
+    """window_edge_batch through both decode_batch_auto instances: status,
+    final context and every written byte against the oracle."""
+    enc, eoff = window_edge_batch()
+    st, _ = auto_decode_check(codec, dev, enc, eoff, "window edges " + pick, pick=pick)
+    assert (st < 0).sum() >= 60  # the invalid encodings do fail
+
+
 @pytest.mark.parametrize("cfg", [2, 3])
 def test_decode_auto_full_size(codec, dev, cfg):
     """BASELINE.json configs 2 / 3 at full size (1M strings) through
