@@ -1432,7 +1432,10 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   if (PAIRS) G2 = min(G2, lim);
   // (SYNC) the last pair: start (as nq), entries, slow code
   uint32_t pb = ~(bp - 1u), le1 = 0, le2 = 0, ls = 0;
-  // (bp = 0: A is the dword before the staged words, never inside a window)
+  // (bp = 0: A is the dword before the staged words, never inside a window;
+  // an LDS read inside the workgroup's shared struct -- the staged words
+  // follow the lookup tables -- so only the LDS reader may come here)
+  static_assert(std::is_same<IN, LdsIn>::value, "dd_run reads index -1: LDS-staged input only");
   int32_t kw = (int32_t)(bp - 1u) >> 5;
   uint32_t A = ib((uint32_t)kw), B = ib((uint32_t)kw + 1u), N = ib((uint32_t)kw + 2u);
   uint32_t nq = ~(bp - 1u);
