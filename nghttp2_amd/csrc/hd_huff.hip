@@ -793,6 +793,7 @@ struct DecT {
   uint32_t long_lim[NLONG_PAD];    // exclusive left-justified limit (last: ~0)
   uint32_t long_delta[NLONG_PAD];  // canonical base - first code (mod 2^32)
   uint32_t long_len[NLONG_PAD];
+  uint32_t long_n1[32];  // leading ones of a window -> its first candidate row
   uint16_t canon[260];
   uint32_t depth_lo[30];
   uint16_t depth_base[30];
@@ -833,6 +834,13 @@ __device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads)
       T.long_delta[i] = T.long_delta[DecT<LB>::NL - 1];
       T.long_len[i] = T.long_len[DecT<LB>::NL - 1];
     }
+  }
+  __syncthreads();
+  if (t < 32) {  // rows below every code with t leading ones (ones, then zeros)
+    const uint32_t wmin = t ? ~0u << (32u - t) : 0u;
+    uint32_t i0 = 0;
+    for (uint32_t r = 0; r < DecT<LB>::NL; ++r) i0 += T.long_lim[r] <= wmin ? 1u : 0u;
+    T.long_n1[t] = min(i0, DecT<LB>::NL - 1u);
   }
   __syncthreads();
 }
@@ -951,10 +959,13 @@ struct CheckedDwordSink {
 // (cnt 1, used = L), or ~0u when EOS (symbol 256) completes within `rem`.
 template <class TT>
 __device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32_t rem) {
-  uint32_t i = 0;
-#pragma unroll
-  for (uint32_t step = NLONG_PAD / 2; step; step >>= 1)
-    i += (T.long_lim[i + step - 1] <= win) ? step : 0u;
+  // the window's leading ones leave at most three candidate lengths (HPACK's
+  // codes past 16 bits): the first candidate row from long_n1, then two
+  // compares (limits are nondecreasing) -- two dependent reads, not four
+  const uint32_t n1 = min((uint32_t)__clz((int)~win), 31u);
+  uint32_t i = T.long_n1[n1];
+  const uint32_t l0 = T.long_lim[i], l1 = T.long_lim[min(i + 1u, NLONG_PAD - 1u)];
+  i += (l0 <= win ? 1u : 0u) + (l1 <= win ? 1u : 0u);
   i = min(i, TT::NL - 1u);  // win == ~0: the 30-bit row
   const uint32_t L = T.long_len[i];
   const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
