@@ -407,6 +407,101 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *co
                                   const uint32_t *block_nv_off, uint8_t *out, size_t out_cap,
                                   uint32_t *out_off, int32_t *block_status, void *stream);
 
+/* ------------------------------------------------------------------ */
+/* One batch over several GPUs                       */
+/* ------------------------------------------------------------------ */
+/*
+ * Strings are independent, so a batch shards into contiguous string ranges
+ * balanced by bytes, one per device, with no exchange between devices (no
+ * RCCL, xGMI unused).  A sharded engine owns one host worker thread, one HIP
+ * stream and its own device buffers per entry of its device list (a device
+ * may repeat: several shards on one GPU); the table of each kernel is staged
+ * per device.  This is nghttp2's concurrency model (one session per thread,
+ * nothing shared; doc/programmers-guide.rst:35-40) with a GPU behind each
+ * thread.  A sharded engine is used by one caller thread at a time; distinct
+ * engines may run concurrently.
+ *
+ * The shard outputs are merged into one batch: shard k's output bytes follow
+ * shard k-1's, and its offsets are rebased by the bytes before it.  Encode:
+ * the result equals nghttp2_amd_hd_huff_encode_batch of the whole batch.
+ * Decode: each shard is laid out as nghttp2_amd_hd_huff_decode_batch_auto
+ * lays out a batch of its strings (dense per task, counted from the shard's
+ * first string), shifted by the bytes of the shards before it; dst_off,
+ * status, fstate and flags are per string as for the unsharded call.
+ */
+typedef struct nghttp2_amd_hd_sharded nghttp2_amd_hd_sharded;
+
+/* Byte-balanced contiguous cut of a batch of n strings (offsets off[n+1])
+ * into nshards ranges: cuts[0] = 0, cuts[nshards] = n, shard k holds the
+ * strings [cuts[k], cuts[k+1]), which start at or after its 1/nshards share
+ * of the bytes.  Host-only.  Returns 0 or NGHTTP2_AMD_ERR_INVALID_ARGUMENT. */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_shard_bounds(const uint32_t *off, uint32_t n, uint32_t nshards,
+                                                   uint32_t *cuts);
+
+/* A sharded engine over ndevices HIP device ids (repeats allowed).  Returns
+ * 0, NGHTTP2_AMD_ERR_INVALID_ARGUMENT (no device, an id out of range) or
+ * NGHTTP2_AMD_ERR_FATAL / _NOMEM (a stream or thread could not be made). */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_sharded_new(nghttp2_amd_hd_sharded **out, const int *devices,
+                                                  uint32_t ndevices);
+NGHTTP2_AMD_EXTERN void nghttp2_amd_hd_sharded_del(nghttp2_amd_hd_sharded *s);
+NGHTTP2_AMD_EXTERN uint32_t nghttp2_amd_hd_sharded_count(const nghttp2_amd_hd_sharded *s);
+
+/*
+ * Host-resident batch (pinned memory gives the full PCIe rate; pageable
+ * memory works and copies through the runtime's staging).  src must be
+ * readable to align_up(src_off[n], 16) + 16 (the pool padding of every batch
+ * call).  Each shard: H2D of its bytes and offsets, the engine kernels, D2H
+ * of its output straight to its merged position.  Synchronous: returns when
+ * every shard's output is in dst.
+ *
+ * encode: Huffman encode; dst_off[n+1] merged (dst_off[0] = 0).  When the
+ *   merged output passes dst_cap or the uint32 offsets, nothing is written to
+ *   dst, dst_off[n] = NGHTTP2_AMD_OFF_OVERFLOW and the call returns
+ *   NGHTTP2_AMD_ERR_BUFFER_ERROR (split the batch).
+ * decode: decode with final=1 (status per string as decode_batch_auto);
+ *   dst_cap >= nghttp2_amd_hd_huff_decode_bound(E, n) + 32 * shards always
+ *   suffices (E = src_off[n] - src_off[0]); a smaller pool that the merged
+ *   output does not fit returns NGHTTP2_AMD_ERR_BUFFER_ERROR with nothing
+ *   written to dst.  fstate and flags may both be NULL.
+ */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_sharded_encode(nghttp2_amd_hd_sharded *s, const uint8_t *src,
+                                                     const uint32_t *src_off, uint32_t n, uint8_t *dst,
+                                                     size_t dst_cap, uint32_t *dst_off);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_sharded_decode(nghttp2_amd_hd_sharded *s, const uint8_t *src,
+                                                     const uint32_t *src_off, uint32_t n, uint8_t *dst,
+                                                     size_t dst_cap, uint32_t *dst_off, int32_t *status,
+                                                     uint16_t *fstate, uint8_t *flags);
+
+/*
+ * Device-resident shards: shards[k] lives on the engine's k-th device (cut
+ * by the caller, e.g. with nghttp2_amd_hd_shard_bounds; its src_off may be
+ * absolute or rebased -- the engine calls take them as given).  Each shard
+ * runs nghttp2_amd_hd_huff_encode_batch / _decode_batch_auto on its device
+ * and stream; its output stays there with shard-local offsets, and the
+ * engine reports out_bytes (its dst_off[n]) and out_base (the bytes of the
+ * shards before it, its position in the merged batch).  Synchronous.
+ * Returns 0 or the first failing shard's error (each shard's own in rv).
+ */
+typedef struct {
+  const uint8_t *src;        /* IN  pool on the shard's device (16-byte aligned, padded) */
+  const uint32_t *src_off;   /* IN  offsets[n+1] on the shard's device */
+  uint32_t n;                /* IN  strings of the shard */
+  uint64_t in_bytes;         /* IN  decode: src_off[n] - src_off[0]; encode: raw bytes */
+  uint8_t *dst;              /* IN  output pool on the shard's device */
+  size_t dst_cap;            /* IN */
+  uint32_t *dst_off;         /* IN  offsets[n+1] on the shard's device */
+  int32_t *status;           /* IN  decode: status[n] on the device (encode: unused) */
+  uint16_t *fstate;          /* IN  decode: optional (with flags) */
+  uint8_t *flags;            /* IN  decode: optional (with fstate) */
+  uint64_t out_bytes;        /* OUT the shard's output bytes (dst_off[n]) */
+  uint64_t out_base;         /* OUT its first byte in the merged batch */
+  int rv;                    /* OUT the shard's nghttp2_error (0) */
+} nghttp2_amd_hd_shard;
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_sharded_encode_dev(nghttp2_amd_hd_sharded *s,
+                                                         nghttp2_amd_hd_shard *shards);
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_sharded_decode_dev(nghttp2_amd_hd_sharded *s,
+                                                         nghttp2_amd_hd_shard *shards);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <atomic>
 #include <type_traits>
 
 #include "../../include/nghttp2_amd_hd.h"
@@ -390,12 +391,14 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
     }
   }
   if (tile_sums) {
-    uint32_t tot, nhuge;
-    // a string whose code bits would not fit the 32-bit counts poisons its
-    // tile's sum (0xFFFFFFFF), so this tile and every one after it overflow
-    // in k_encode
-    block_excl_scan_sum<EC_CNT_NT>(e, huge ? 1u : 0u, red, &tot, &nhuge);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = nhuge ? 0xFFFFFFFFu : tot;
+    uint32_t tot, hi;
+    // a string whose code bits would not fit the 32-bit counts, or a tile
+    // whose output might not fit 32 bits (its sum in 64 KiB units, which
+    // cannot wrap, within 256 units of 2^16: the uint32 total could have
+    // wrapped), poisons its tile's sum (0xFFFFFFFF), so this tile and every
+    // one after it overflow in k_encode
+    block_excl_scan_sum<EC_CNT_NT>(e, huge ? 0x10000u : e >> 16, red, &tot, &hi);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = hi >= 0x10000u - WG ? 0xFFFFFFFFu : tot;
   }
 }
 
@@ -538,7 +541,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   const bool anyraw = FR && __ballot(rawl) != 0;
   // (FR: a wave of empty strings only still has its literals: one round)
   const uint32_t c_stop = FR && c_end == c0 ? c0 + 1u : c_end;
-  uint32_t x = 0;  // output bit of the round's first wave byte (relative to G0)
+  uint64_t x = 0;  // output bit of the round's first wave byte (relative to G0; a wave's
+                   // output may pass 2^32 bits)
   for (uint32_t cb = c0; cb < c_stop; cb += 64u) {
     const bool first = cb == c0, last_round = cb + 64u >= c_stop;
     const uint32_t base = cb << 4;
@@ -709,7 +713,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- store whole words and zero them; carry a partial last word
-    const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) + X0 - RA;
+    const uint64_t xe = last_round ? 8ull * (OZ - OA)
+                                   : x + (uint64_t)__builtin_amdgcn_readlane(Sinc, 63) + X0 - RA;
     const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
     const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
     // words [ilo, ihi) lie inside the wave's output [OA, OZ) (<= dst_cap by
@@ -1310,6 +1315,17 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
                    // round 3 with overshooting warm-ups, 16/18/22: 312.4/308.9/304.8 vs 300.8)
 #define DD_TASK_W 32u  // a string's weight in bytes when balancing tasks over workgroups
 #define DD_NONE 0xFFFFFFFCu  // a round's carried exit: the last item ended its string
+#ifdef DD_ABL_NOOUT
+#define DD_NOOUT_ON true
+#else
+#define DD_NOOUT_ON false
+#endif
+#ifndef DD_IW40
+#define DD_IW40 16
+#endif
+#ifndef DD_SK40
+#define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)
+#endif
 
 // Decode symbols into a byte stream in LDS: both bytes of an entry are
 // written, the count advances by the entry's symbols.
@@ -1335,7 +1351,11 @@ template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
 struct DIShared {  // k_decode_items
   DecT<LB> T;  // first: the lookup at LDS offset 0
   alignas(16) uint32_t ib[IW][di_ibw(di_span(IP, BI))];
+#ifdef DD_ABL_NOOUT
+  alignas(16) uint32_t ob[IW][4];
+#else
   alignas(16) uint32_t ob[IW][(di_obb(IP, BI) / 4 + 1 + 3) & ~3u];
+#endif
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
   uint32_t claimed;               // tasks of the workgroup's range claimed so far
@@ -1359,8 +1379,12 @@ struct LdsPtrSink {
     // (round 3: one ds_write_b16 at the byte address -- the LDS runs in
     // unaligned mode, tools/diag/probe -- measured slower: 354.9 vs 296.2 us
     // on config 3, the hardware splits misaligned stores)
+#ifndef DD_ABL_NOOUT
     p[0] = (uint8_t)v;
     p[1] = (uint8_t)(v >> 16);
+#else
+    (void)v;
+#endif
     p += c8 >> 3;
   }
   __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
@@ -1423,7 +1447,7 @@ struct DDRun {
 // PAIRS: only the fast pairs, none starting past `lim` (no careful steps):
 // bp stops at a codeword boundary on the way, for a caller that records it
 // and goes on with another dd_run.
-template <class Sink, bool SYNC = false, bool PAIRS = false, class TT, class IN>
+template <class Sink, bool SYNC = false, bool PAIRS = false, uint32_t SLOWK = 1, class TT, class IN>
 __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
                                         int32_t lim = INT32_MAX) {
@@ -1431,7 +1455,7 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   r.at_end = false;
   r.t = 0;
   r.win = 0;
-  bool failed = false;
+  uint32_t failed = 0;  // (a VGPR flag: a lane-mask bool costs SALU merges every pair)
 
   // last start of a fast pair: every code it takes starts before bstop (the
   // second step's second symbol at most LB + (LB - 5) bits on) and ends
@@ -1456,27 +1480,34 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   // a code longer than the lookup inside the pair loop: decode it, or leave
   // the pair loop at EOS (failed) or at the string's tail (the careful steps
-  // find it again)
+  // find it again).  Predicated, with `failed` a VGPR flag: the nested
+  // branches this replaces left exec-mask merges (≈7 SALU) in every pair,
+  // taken or not (round 4: config 3 decode 277.6 -> 258.1 us, config 5
+  // 135.1 -> 130.0, config 2 48.8 -> 47.8).  SLOWK > 1: a lane that meets a
+  // long code stalls (its entries use no bits and emit nothing) and the
+  // long codes are served every SLOWK-th pair, so the wave pays the slow
+  // path's dependent reads once for several lanes' codes (config 3, k = 2:
+  // 258.1 -> 253.0 us; the 64-byte instance, which serves config 5's 30-bit
+  // codes everywhere, keeps k = 1)
 #define DD_SLOW()                                                        \
   do {                                                                   \
     const uint32_t rem_ = bend - (~nq + 1u);                             \
     const uint32_t e_ = slow_entry(T, __builtin_amdgcn_alignbit(A, B, nq), rem_); \
-    if (e_ == 0xFFFFFFFFu) {                                             \
-      failed = true;                                                     \
-      nG = INT32_MAX;                                                    \
-    } else if (E_L1(e_) > rem_) {                                        \
-      nG = INT32_MAX;                                                    \
-    } else {                                                             \
-      sink.put(e_ & E_OUT2, E_CNT8(e_));                                 \
-      const uint32_t U_ = E_USED(e_);                                    \
-      if (SYNC) ls = U_;                                                 \
-      DD_ADV(U_);                                                        \
-    }                                                                    \
+    const bool eos_ = e_ == 0xFFFFFFFFu;                                 \
+    const bool ok_ = !eos_ && E_L1(e_) <= rem_;                          \
+    failed |= eos_ ? 1u : 0u;                                            \
+    nG = ok_ ? nG : INT32_MAX;                                           \
+    const uint32_t ek_ = ok_ ? e_ : 0u;                                  \
+    sink.put(ek_ & E_OUT2, E_CNT8(ek_));                                 \
+    const uint32_t U_ = E_USED(ek_);                                     \
+    if (SYNC) ls = U_;                                                   \
+    DD_ADV(U_);                                                          \
   } while (0)
   // The fast pairs run at raised wave priority: the SIMD issues their
   // dependent chain's VALU before other waves' staging, scans and stores
   // (config 3 decode 294.1 vs 297.7 us, config 2 50.6 vs 52.2; priority 3,
   // or priority over the whole run with its careful steps: no better)
+  uint32_t it = 0;
   __builtin_amdgcn_s_setprio(1);
   while ((int32_t)nq >= nG) {
     const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
@@ -1492,7 +1523,8 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
       ls = 0;
     }
     DD_ADV(U1 + U2);
-    if (e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */
+    ++it;
+    if ((SLOWK == 1u || (it & (SLOWK - 1u)) == 0u) && e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */
   }
   __builtin_amdgcn_s_setprio(0);
 #undef DD_SLOW
@@ -1519,21 +1551,20 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     // steps that take a 2-symbol entry's second symbol only while the first
     // ends before bstop.  EOS, or a code that would pass the string end,
     // leaves the entry unknown (failed; the verify re-decodes the item).
-    bool done = failed || (int32_t)bp >= (int32_t)bstop;
-    while (__ballot(!done)) {
-      if (!done) {
+    // (flags as VGPR words, not lane-mask bools, as in the careful steps)
+    uint32_t done = (failed || (int32_t)bp >= (int32_t)bstop) ? 1u : 0u;
+    while (__ballot(done == 0u)) {
+      if (done == 0u) {
         const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
         uint32_t e = T.lut[w >> (32 - TT::BITS)];
         if (e == 0u) e = slow_entry(T, w, 30u);
         const uint32_t L1 = E_L1(e), adv = bp + L1 >= bstop ? L1 : E_USED(e);
-        if (e == 0xFFFFFFFFu || bp + adv > bend) {
-          failed = true;
-          done = true;
-        } else {
-          bp += adv;
-          DD_ADV(adv);
-          done = bp >= bstop;
-        }
+        const bool bad = e == 0xFFFFFFFFu || bp + adv > bend;
+        failed |= bad ? 1u : 0u;
+        const uint32_t a = bad ? 0u : adv;
+        bp += a;
+        DD_ADV(a);
+        done = (bad || bp >= bstop) ? 1u : 0u;
       }
     }
     r.failed = failed;
@@ -1546,33 +1577,36 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // -- with every lane stepping (a finished lane takes nothing): selects
   // instead of exec-mask branches, the rare long code behind one uniform
   // branch
-  bool done = failed;
-  {
-    while (__ballot(!done)) {
-      const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
-      const uint32_t rem = bend - bp;
-      const bool stop = done || bp >= bstop || rem == 0u;
-      uint32_t e = T.lut[w >> (32 - TT::BITS)];
-      const bool slow = e == 0u && !stop;
-      if (__ballot(slow)) {
-        if (slow) e = slow_entry(T, w, rem);
-      }
-      const bool eos = e == 0xFFFFFFFFu && !stop;  // EOS: the sticky failure state
-      const uint32_t L1 = E_L1(e), U = E_USED(e);
-      const bool take1 = !stop && !eos && L1 <= rem;
-      const bool take2 = take1 && E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
-      const bool tail = !stop && !eos && !take1;  // a proper prefix of a code
-      r.at_end = r.at_end || tail;
-      r.t = tail ? rem : r.t;
-      r.win = tail ? w : r.win;
-      const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
-      sink.put(take2 ? (e & E_OUT2) : (take1 ? (e & E_OUT1) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
-      bp += adv;
-      DD_ADV(adv);
-      failed = failed || eos;
-      done = done || eos || !take1 || bp >= bstop;
+  // (the loop-carried flags are VGPR words: as lane-mask bools every merge
+  // of them costs SALU in each step)
+  uint32_t done = failed, at_end = 0u, tt = 0u, twin = 0u;
+  while (__ballot(done == 0u)) {
+    const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
+    const uint32_t rem = bend - bp;
+    const bool stop = done != 0u || bp >= bstop || rem == 0u;
+    uint32_t e = T.lut[w >> (32 - TT::BITS)];
+    const bool slow = e == 0u && !stop;
+    if (__ballot(slow)) {
+      if (slow) e = slow_entry(T, w, rem);
     }
+    const bool eos = e == 0xFFFFFFFFu && !stop;  // EOS: the sticky failure state
+    const uint32_t L1 = E_L1(e), U = E_USED(e);
+    const bool take1 = !stop && !eos && L1 <= rem;
+    const bool take2 = take1 && E_CNT(e) == 2u && U <= rem && bp + L1 < bstop;
+    const bool tail = !stop && !eos && !take1;  // a proper prefix of a code
+    at_end |= tail ? 1u : 0u;
+    tt = tail ? rem : tt;
+    twin = tail ? w : twin;
+    const uint32_t adv = take2 ? U : (take1 ? L1 : 0u);
+    sink.put(take2 ? (e & E_OUT2) : (take1 ? (e & E_OUT1) : 0u), take2 ? 16u : (take1 ? 8u : 0u));
+    bp += adv;
+    DD_ADV(adv);
+    failed |= eos ? 1u : 0u;
+    done |= (eos || !take1 || bp >= bstop) ? 1u : 0u;
   }
+  r.at_end = at_end != 0u;
+  r.t = tt;
+  r.win = twin;
   sink.flush();
   if (!failed && bp == bend) r.at_end = true;
   r.failed = failed;
@@ -1612,7 +1646,7 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
-template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1>
 __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
                                                         const uint32_t *__restrict__ off,
                                                         uint32_t n, uint8_t *__restrict__ dst,
@@ -1831,7 +1865,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       if (spec) {
         uint32_t bp = 8u * (s - DD_OV - IBX);
         DiscardSink dk;
-        const DDRun rw = dd_run<DiscardSink, true>(S.T, inp, bp, bs, bend, dk);
+        const DDRun rw = dd_run<DiscardSink, true, false, SK>(S.T, inp, bp, bs, bend, dk);
         entry = bp;
         dead = rw.failed;
       }
@@ -1843,7 +1877,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // (kMerge: the item is decoded in the verify loop's first pass, by the
       // same inlined decoder as its re-decodes)
       constexpr bool kMerge = BI == 0;
-      if (valid && !dead && !kMerge) rr = dd_run(S.T, inp, bp, bstop, bend, sk);
+      if (valid && !dead && !kMerge) rr = dd_run<DISink, false, false, SK>(S.T, inp, bp, bstop, bend, sk);
       uint32_t my_exit = rr.failed ? XFAIL : bp;
       uint32_t my_entry = dead ? XUNKNOWN : entry;
       uint32_t c0 = sk.count();
@@ -1857,7 +1891,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           if (run_) {
             DISink s3(my_ob);
             uint32_t bq = start;
-            rr = dd_run(S.T, inp, bq, bstop, bend, s3);
+            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3);
             my_exit = rr.failed ? XFAIL : bq;
             c0 = s3.count();
           }
@@ -1882,7 +1916,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             run_ = true;
           } else {
             uint32_t bq = pred;
-            rr = dd_run(S.T, inp, bq, bstop, bend, s3);
+            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3);
             my_exit = rr.failed ? XFAIL : bq;
             c0 = s3.count();
           }
@@ -1904,7 +1938,11 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- dense placement
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
+#ifdef DD_ABL_NOOUT
+      if (false) {
+#else
       if (IP >= 64u) {
+#endif
         // The round's bytes are the task's output [R0g, R1g): each lane moves
         // its region into the round's global dwords [W0, W1), laid out back
         // to back over the regions (realigned by alignbyte; the words shared
@@ -1981,7 +2019,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           }
         }
         ocarry = (!lastr && nst < nwr) ? __builtin_amdgcn_readfirstlane(D[nst]) : 0u;
-      } else {
+      } else if (!DD_NOOUT_ON) {
         // dwords realigned to the output (alignbyte) for as many dwords as
         // the wave's longest region, four per step; the bytes before the
         // first aligned dword and after the last one stored singly
@@ -2129,20 +2167,30 @@ __global__ __launch_bounds__(WG) void k_copy_calib(uint4 *__restrict__ dst,
 // x CU count, cached per kernel), so no workgroup runs as a second "wave"
 // and the LDS tables are staged once per resident workgroup.
 template <class K>
-static uint32_t resident_blocks(K kernel, int BS) {
-  int dev = 0, cus = NUM_CU, per = DEC_WG_PER_CU;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+static uint32_t resident_blocks(K kernel, int BS, int dev) {
+  int cus = NUM_CU, per = DEC_WG_PER_CU;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, BS, 0) != hipSuccess || per < 1)
     per = 1;
   return (uint32_t)(cus * per);
 }
+// The resident count is cached per kernel and per device (the caller's
+// current device): host threads driving different GPUs (or the same one)
+// may launch concurrently, so the cache is atomic -- a race only computes
+// the same value twice.
+#define HD_MAX_DEVICES 64
 template <auto KERNEL, int BS, int UNIT = BS>  // UNIT: items per workgroup task
 static uint32_t persistent_grid(uint32_t n) {
-  static uint32_t cap = 0;  // one per kernel
-  if (cap == 0) cap = resident_blocks(KERNEL, BS);
+  static std::atomic<uint32_t> cap[HD_MAX_DEVICES];  // zero-initialised (static storage)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  uint32_t c = dev < HD_MAX_DEVICES ? cap[dev].load(std::memory_order_relaxed) : 0u;
+  if (c == 0) {
+    c = resident_blocks(KERNEL, BS, dev);
+    if (dev < HD_MAX_DEVICES) cap[dev].store(c, std::memory_order_relaxed);
+  }
   const uint32_t g = (n + UNIT - 1) / UNIT;
-  return g < cap ? g : cap;
+  return g < c ? g : c;
 }
 
 static int hip_rv(hipError_t e) {
@@ -2152,13 +2200,13 @@ static int hip_rv(hipError_t e) {
 }
 
 #ifndef HD_PART_ENC
-template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1>
 static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
                                 uint8_t *dst, size_t dst_cap, uint32_t *dst_off,
                                 int32_t *status, uint16_t *fstate, uint8_t *flags,
                                 hipStream_t st) {
-  hipLaunchKernelGGL((k_decode_items<IP, IW, LB, BI>),
-                     dim3(persistent_grid<k_decode_items<IP, IW, LB, BI>, WAVE * IW, TASK_STR * IW>(n)),
+  hipLaunchKernelGGL((k_decode_items<IP, IW, LB, BI, SK>),
+                     dim3(persistent_grid<k_decode_items<IP, IW, LB, BI, SK>, WAVE * IW, TASK_STR * IW>(n)),
                      dim3(WAVE * IW), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off,
                      status, fstate, flags);
 }
@@ -2189,7 +2237,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (enc_bytes <= 48ull * n)
     launch_decode_items<64u, 16, 13, 2304u>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
-    launch_decode_items<40u, 16, 13>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<40u, DD_IW40, 13, 0u, DD_SK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
 }
 

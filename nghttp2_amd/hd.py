@@ -249,15 +249,19 @@ class HuffmanBatchCodec:
                     want_ctx=False, stream=None, pick=None):
         """Decode into a dense pool (one launch): the strings of each task of
         64 consecutive strings back to back from the task's base
-        auto_slot(x_t0, t0).  enc_bytes = src_off[n] - src_off[0] (default: the
-        pool size, an upper bound) sizes dst and picks the kernel instance by
-        the mean string length; pick = "items64" / "pieces40" forces one
-        instance through that same argument (tests).  Returns
+        auto_slot(x_t0, t0).  enc_bytes = src_off[n] - src_off[0] sizes dst and
+        picks the kernel instance by the mean string length; when it is not
+        given it is read from src_off on the call's stream (a host
+        synchronisation of that stream: pass it to keep the call
+        asynchronous).  pick = "items64" / "pieces40" forces one instance
+        through that same argument (tests).  Returns
         (dst, dst_off, status[, fstate, flags])."""
         torch = self.torch
         n = src_off.numel() - 1
         if enc_bytes is None:
-            enc_bytes = src.numel()
+            with torch.cuda.stream(self._on(stream)):
+                ends = src_off[[0, n]].cpu().numpy().view("uint32").astype("int64")
+            enc_bytes = int(ends[1] - ends[0])
         sel = {None: int(enc_bytes), "items64": 0, "pieces40": 49 * max(1, n)}[pick]
         if dst is None:
             dst = self._empty(self.decode_bound(enc_bytes, n), torch.uint8, stream)

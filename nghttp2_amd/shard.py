@@ -50,110 +50,101 @@ def merge(parts):
             np.concatenate(offs).astype(np.uint64))
 
 
+def _lib():
+    import ctypes
+    from .hd import lib
+    L = lib()
+    if not getattr(L, "_sharded_bound", False):
+        vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+        L.nghttp2_amd_hd_shard_bounds.argtypes = [vp, u32, u32, vp]
+        L.nghttp2_amd_hd_sharded_new.argtypes = [ctypes.POINTER(vp), vp, u32]
+        L.nghttp2_amd_hd_sharded_del.argtypes = [vp]
+        L.nghttp2_amd_hd_sharded_del.restype = None
+        L.nghttp2_amd_hd_sharded_count.argtypes = [vp]
+        L.nghttp2_amd_hd_sharded_count.restype = u32
+        L.nghttp2_amd_hd_sharded_encode.argtypes = [vp, vp, vp, u32, vp, sz, vp]
+        L.nghttp2_amd_hd_sharded_decode.argtypes = [vp, vp, vp, u32, vp, sz, vp, vp, vp, vp]
+        L._sharded_bound = True
+    return L
+
+
+def _ptr(a):
+    import ctypes
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _padded(pool, end):
+    """The pool readable to align_up(end, 16) + 16, as every batch call needs."""
+    need = end + (-end) % 16 + 16
+    pool = np.ascontiguousarray(pool, dtype=np.uint8)
+    if pool.size >= need:
+        return pool
+    out = np.zeros(need, dtype=np.uint8)
+    out[:pool.size] = pool
+    return out
+
+
 class ShardedCodec:
-    """One batch over several devices in ONE process: the
-    batch is cut into byte-balanced contiguous shards, one per entry of
-    `devices`; each shard runs on its own host thread with its own HIP stream
-    and its own HuffmanBatchCodec, and the host rebases the shards' output
-    offsets into one batch (`merge`).  This is the reference's threading
+    """One batch over several devices in ONE process, through
+    the library's sharded engine (include/nghttp2_amd_hd.h
+    nghttp2_amd_hd_sharded_*): the batch is cut into byte-balanced contiguous
+    shards, one per entry of `devices`; each shard runs on the engine's
+    worker thread for its device, with its own HIP stream and device buffers
+    (H2D, the kernels, D2H straight to the merged position), and the shards'
+    offsets are rebased into one batch.  This is the reference's threading
     model (doc/programmers-guide.rst:36-40: one nghttp2 session per thread,
-    no shared state) with a device behind each thread.  No collective: the
-    shards never exchange data.
+    no shared state) with a device behind each thread, in native code.  No
+    collective: the shards never exchange data.
 
     `devices` may repeat a device (e.g. [0, 0]: two shards, two threads and
-    two streams on one GPU).  Inputs and merged outputs are host numpy
-    arrays; the device parts stay available from the last call
-    (`last_parts`) for callers that keep the results resident."""
+    two streams on one GPU).  Inputs and outputs are host numpy arrays."""
 
     def __init__(self, devices):
-        import threading
-        import torch
-
-        from .hd import HuffmanBatchCodec
-        self.torch = torch
-        self.devices = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d)
-                        for d in devices]
+        import ctypes
+        self.devices = [d if isinstance(d, int) else (d.index or 0) for d in devices]
         if not self.devices:
             raise ValueError("ShardedCodec needs at least one device")
-        self.codecs, self.streams = [], []
-        for d in self.devices:
-            with torch.cuda.device(d):
-                self.codecs.append(HuffmanBatchCodec(d))
-                self.streams.append(torch.cuda.Stream(device=d))
-        self._lock = threading.Lock()
-        self.last_parts = None
+        self.L = _lib()
+        h = ctypes.c_void_p()
+        ids = (ctypes.c_int * len(self.devices))(*self.devices)
+        rv = self.L.nghttp2_amd_hd_sharded_new(ctypes.byref(h), ids, len(self.devices))
+        if rv != 0:
+            raise RuntimeError("nghttp2_amd: sharded_new failed with nghttp2 error %d" % rv)
+        self.h = h
 
-    def _run(self, fn, n):
-        """fn(k) for every shard k, each on its own host thread; re-raises the
-        first failure after every thread has finished."""
-        import threading
-        out, err = [None] * n, []
-
-        def body(k):
-            try:
-                with self.torch.cuda.device(self.devices[k]), \
-                        self.torch.cuda.stream(self.streams[k]):
-                    out[k] = fn(k)
-                    self.streams[k].synchronize()
-            except BaseException as e:  # reported after the join
-                with self._lock:
-                    err.append((k, e))
-        ts = [threading.Thread(target=body, args=(k,)) for k in range(n)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        if err:
-            k, e = sorted(err, key=lambda x: x[0])[0]
-            raise RuntimeError("shard %d (%s) failed: %s" % (k, self.devices[k], e)) from e
-        return out
-
-    def _scatter(self, pool, off):
-        off = np.asarray(off, dtype=np.int64)
-        bounds = byte_balanced_bounds(off, len(self.devices))
-        return bounds, [shard(pool, off, s0, s1) for s0, s1 in bounds]
-
-    def _to_dev(self, k, sp, so):
-        t = self.torch
-        src = t.from_numpy(sp).to(self.devices[k], non_blocking=False)
-        src_off = t.from_numpy(so.astype(np.uint32).view(np.int32)).to(self.devices[k])
-        return src, src_off
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.nghttp2_amd_hd_sharded_del(self.h)
+            self.h = None
 
     def encode(self, pool, off):
         """Huffman-encode the batch across the devices: returns the merged
         (encoded pool uint8, offsets uint64[n+1]), equal to a single-device
         encode of the whole batch."""
-        _, parts = self._scatter(pool, off)
-
-        def work(k):
-            sp, so = parts[k]
-            src, src_off = self._to_dev(k, sp, so)
-            enc, eoff = self.codecs[k].encode(src, src_off, raw_bytes=int(so[-1]),
-                                              stream=self.streams[k])
-            return enc, eoff
-        dev_parts = self._run(work, len(parts))
-        self.last_parts = dev_parts
-        host = [(e.cpu().numpy(), o.cpu().numpy().view(np.uint32)) for e, o in dev_parts]
-        return merge(host)
+        from .hd import _check
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        src = _padded(pool, int(off[-1]))
+        cap = self.L.nghttp2_amd_hd_huff_encode_bound(int(off[-1]) - int(off[0]), n)
+        dst = np.empty(cap, dtype=np.uint8)
+        doff = np.empty(n + 1, dtype=np.uint32)
+        _check(self.L.nghttp2_amd_hd_sharded_encode(self.h, _ptr(src), _ptr(off), n, _ptr(dst), cap,
+                                                    _ptr(doff)), "sharded_encode")
+        return dst[:int(doff[-1])], doff.astype(np.uint64)
 
     def decode_auto(self, enc_pool, enc_off):
-        """Decode the batch (final=1 per string) across the devices into the
-        dense layout of each shard, merged: returns (decoded pool uint8,
-        dst_off uint64[n+1], status int32[n]); string i's bytes are
+        """Decode the batch (final=1 per string) across the devices, each
+        shard in decode_batch_auto's dense layout, merged: returns (decoded
+        pool uint8, dst_off uint64[n+1], status int32[n]); string i's bytes are
         pool[dst_off[i] : dst_off[i] + status[i]] when status[i] >= 0."""
-        _, parts = self._scatter(enc_pool, enc_off)
-
-        def work(k):
-            sp, so = parts[k]
-            src, src_off = self._to_dev(k, sp, so)
-            return self.codecs[k].decode_auto(src, src_off, enc_bytes=int(so[-1]),
-                                              stream=self.streams[k])
-        dev_parts = self._run(work, len(parts))
-        self.last_parts = dev_parts
-        host, status = [], []
-        for d, o, st in dev_parts:
-            oh = o.cpu().numpy().view(np.uint32)
-            host.append((d[:int(oh[-1])].cpu().numpy(), oh))
-            status.append(st.cpu().numpy())
-        pool_m, off_m = merge(host)
-        return pool_m, off_m, (np.concatenate(status) if status else np.zeros(0, np.int32))
+        from .hd import _check
+        off = np.ascontiguousarray(enc_off, dtype=np.uint32)
+        n = len(off) - 1
+        src = _padded(enc_pool, int(off[-1]))
+        cap = self.L.nghttp2_amd_hd_huff_decode_bound(int(off[-1]) - int(off[0]), n) + 32 * len(self.devices)
+        dst = np.empty(cap, dtype=np.uint8)
+        doff = np.empty(n + 1, dtype=np.uint32)
+        st = np.empty(max(1, n), dtype=np.int32)
+        _check(self.L.nghttp2_amd_hd_sharded_decode(self.h, _ptr(src), _ptr(off), n, _ptr(dst), cap,
+                                                    _ptr(doff), _ptr(st), None, None), "sharded_decode")
+        return dst[:int(doff[-1])], doff.astype(np.uint64), st[:n]

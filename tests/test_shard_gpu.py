@@ -22,7 +22,7 @@ def test_sharded_encode_equals_unsharded_oracle(dev, nshards):
     ref, roff = O.encode_batch(pool, off)
     assert np.array_equal(eoff, roff.astype(np.uint64)), "merged offsets"
     assert np.array_equal(enc, ref), "merged encoded bytes"
-    assert len(sc.last_parts) == nshards
+
 
 
 @pytest.mark.parametrize("kind", ["mixed", "adversarial"])
