@@ -181,6 +181,12 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+// byte-aligned views for unaligned global stores (gfx950 takes them whole)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x4 __attribute__((aligned(1))) u32x4u;
+typedef u32x2 __attribute__((aligned(1))) u32x2u;
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint16_t __attribute__((aligned(1))) u16u;
 
 // Word writer for encode output: the stream [o, o+E) receives big-endian
 // 32-bit groups; with phase = o & 3 fixed, each group completes one aligned
@@ -1315,10 +1321,16 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
                    // round 3 with overshooting warm-ups, 16/18/22: 312.4/308.9/304.8 vs 300.8)
 #define DD_TASK_W 32u  // a string's weight in bytes when balancing tasks over workgroups
 #define DD_NONE 0xFFFFFFFCu  // a round's carried exit: the last item ended its string
-#ifdef DD_ABL_NOOUT
+#if defined(DD_ABL_NOOUT) || defined(DD_ABL_NOSTORE)
 #define DD_NOOUT_ON true
 #else
 #define DD_NOOUT_ON false
+#endif
+#ifndef DD_UST40
+#define DD_UST40 true
+#endif
+#ifndef DD_UST64
+#define DD_UST64 true
 #endif
 #ifndef DD_IW40
 #define DD_IW40 16
@@ -1938,10 +1950,53 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- dense placement
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
-#ifdef DD_ABL_NOOUT
+      constexpr bool kUst = IP >= 64u ? DD_UST64 : DD_UST40;
+#if defined(DD_ABL_NOOUT) || defined(DD_ABL_NOSTORE)
       if (false) {
 #else
-      if (IP >= 64u) {
+      if (kUst) {
+        // each lane stores its region straight to its output bytes with
+        // unaligned stores (gfx950 global memory takes them whole): 16-byte
+        // pieces, then the tail as 8-, 4-, 2- and 1-byte pieces -- no
+        // realignment and no byte-wise head
+        const uint64_t g0 = tbase + O_l;
+        const bool fits = g0 + V <= dst_cap;
+        const uint32_t n16 = fits ? V >> 4 : 0u;
+        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(n16), 63);
+        uint8_t *o = dst + g0;
+#pragma unroll
+        for (uint32_t m = 0; m < (di_rb(IP) + 15u) / 16u; ++m) {
+          if (m >= mx) break;
+          if (m < n16) {
+            u32x4 v;
+            v.x = my_ob32[4u * m];
+            v.y = my_ob32[4u * m + 1u];
+            v.z = my_ob32[4u * m + 2u];
+            v.w = my_ob32[4u * m + 3u];
+            *(u32x4u *)(o + 16u * m) = v;
+          }
+        }
+        if (fits) {
+          const uint32_t t = V & 15u;
+          uint32_t b = V & ~15u;
+          if (t & 8u) {
+            *(u32x2u *)(o + b) = u32x2{my_ob32[b >> 2], my_ob32[(b >> 2) + 1u]};
+            b += 8u;
+          }
+          if (t & 4u) {
+            *(u32u *)(o + b) = my_ob32[b >> 2];
+            b += 4u;
+          }
+          if (t & 2u) {
+            *(u16u *)(o + b) = (uint16_t)(my_ob32[b >> 2] >> (8u * (b & 2u)));
+            b += 2u;
+          }
+          if (t & 1u) o[b] = my_ob[b];
+        } else {  // near dst_cap: byte by byte, nothing at or past it
+          for (uint32_t x = 0; x < V; ++x)
+            if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
+        }
+      } else if (IP >= 64u) {
 #endif
         // The round's bytes are the task's output [R0g, R1g): each lane moves
         // its region into the round's global dwords [W0, W1), laid out back

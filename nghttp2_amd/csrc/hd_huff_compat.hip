@@ -5,13 +5,28 @@
 // Each call is a batch of one string through the batched device API of
 // hd_huff.hip (encode_count / encode kernels, and the reference nibble-FSM
 // kernel for decode so a chunked string resumes from its carried context).
-// One process-wide engine (stream, device buffers, pinned staging) serves
-// all callers under a mutex.
+//
+// Threading follows nghttp2's model (doc/programmers-guide.rst:35-40: one
+// session per thread, nothing shared): every calling host thread gets its
+// own engine -- HIP stream, device buffer, pinned staging -- on the device
+// current in that thread at its first call, so concurrent callers never
+// serialise on a lock or a stream.  A call is one round trip: one H2D of
+// the string and its metadata from one pinned block, the kernels, one D2H
+// of the results and output bytes into it, one synchronisation.
+//
+// emit_string (lib/nghttp2_hd.c:1009, :1037) asks for the count and then,
+// when Huffman wins, for the encoding of the same bytes.  The count runs the
+// whole encode and keeps its output (and a copy of the input) in the
+// thread's engine; an encode of the same bytes right after it takes the kept
+// output without a second round trip (its input is compared byte for byte,
+// so a caller that changed the bytes in between gets a fresh encode).
 #include <hip/hip_runtime.h>
-#include <mutex>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <new>
+#include <vector>
 
 #include "../../include/nghttp2_amd_hd.h"
 #include "../../include/nghttp2_amd_hd_huffman_compat.h"
@@ -19,24 +34,6 @@
 extern "C" int nghttp2_bufs_addb(nghttp2_bufs *bufs, uint8_t b) __attribute__((weak));
 
 namespace {
-
-struct Single {
-  std::mutex mu;
-  bool ready = false, failed = false;
-  hipStream_t st = nullptr;
-  uint8_t *d_in = nullptr, *d_out = nullptr, *h_pin = nullptr;
-  size_t in_cap = 0, out_cap = 0, pin_cap = 0;
-  uint32_t *d_meta = nullptr;  // [0..1] in off, [2..3] out off, [4] status, [5] count
-  uint16_t *d_fs = nullptr;
-  uint8_t *d_fl = nullptr;
-  void *d_ws = nullptr;
-  size_t ws = 0;
-};
-
-Single &eng() {
-  static Single s;
-  return s;
-}
 
 bool hip_ok(hipError_t e) {
   if (e == hipSuccess) return true;
@@ -46,51 +43,105 @@ bool hip_ok(hipError_t e) {
 
 size_t round16(size_t x) { return (x + 15u) & ~size_t(15); }
 
-// grow device / pinned buffers; all sizes include the 16-byte read padding
-bool reserve(Single &s, size_t in_bytes, size_t out_bytes) {
-  if (!s.ready) {
-    if (s.failed) return false;
-    s.failed = true;
-    if (!hip_ok(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking))) return false;
-    if (!hip_ok(hipMalloc(&s.d_meta, 64))) return false;
-    if (!hip_ok(hipMalloc(&s.d_fs, 16)) || !hip_ok(hipMalloc(&s.d_fl, 16))) return false;
-    s.ws = nghttp2_amd_hd_huff_workspace_size(1);
-    if (!hip_ok(hipMalloc(&s.d_ws, s.ws)) || !hip_ok(hipMemset(s.d_ws, 0, s.ws))) return false;
-    s.failed = false;
-    s.ready = true;
+// Layout of one call (device buffer and pinned block alike):
+//   [in: string bytes, round16(len) + 16][meta: 64 B][res: 16 B][out bytes]
+// meta: u32 src_off[2] | u32 dst_off[2] | u16 init fstate | u8 init flags
+// res:  encode: u32 enc_off[2];  decode: i32 status | u16 fstate | u8 flags
+struct Layout {
+  size_t meta, res, out, total;
+  Layout(size_t len, size_t out_cap) {
+    meta = round16(len) + 16;
+    res = meta + 64;
+    out = res + 16;
+    total = out + round16(out_cap) + 16;
   }
-  in_bytes = round16(in_bytes) + 32;
-  out_bytes = round16(out_bytes) + 32;
-  if (in_bytes > s.in_cap) {
-    if (s.d_in) (void)hipFree(s.d_in);
-    s.d_in = nullptr;
-    if (!hip_ok(hipMalloc(&s.d_in, in_bytes))) return false;
-    s.in_cap = in_bytes;
+};
+
+struct Engine {
+  bool ready = false;
+  int device = -1;
+  hipStream_t st = nullptr;
+  uint8_t *d_buf = nullptr, *h_pin = nullptr;
+  size_t cap = 0;
+  void *d_ws = nullptr;
+  size_t ws = 0;
+  // the last count's full encode (emit_string's count -> encode pair)
+  bool kept = false;
+  std::vector<uint8_t> kept_src, kept_out;
+
+  ~Engine() {
+    if (!ready) return;
+    if (d_buf) (void)hipFree(d_buf);
+    if (h_pin) (void)hipHostFree(h_pin);
+    if (d_ws) (void)hipFree(d_ws);
+    if (st) (void)hipStreamDestroy(st);
   }
-  if (out_bytes > s.out_cap) {
-    if (s.d_out) (void)hipFree(s.d_out);
-    s.d_out = nullptr;
-    if (!hip_ok(hipMalloc(&s.d_out, out_bytes))) return false;
-    s.out_cap = out_bytes;
+  // the thread's stream and buffers on its current device; grows to `need`
+  bool reserve(size_t need) {
+    int dev = 0;
+    if (!hip_ok(hipGetDevice(&dev))) return false;
+    if (ready && dev != device) {  // the thread moved to another device
+      this->~Engine();
+      new (this) Engine();
+    }
+    if (!ready) {
+      device = dev;
+      if (!hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking))) return false;
+      ws = nghttp2_amd_hd_huff_workspace_size(1);
+      if (!hip_ok(hipMalloc(&d_ws, ws))) return false;
+      ready = true;
+    }
+    if (need > cap) {
+      need = round16(need) + 4096;
+      if (d_buf) (void)hipFree(d_buf);
+      if (h_pin) (void)hipHostFree(h_pin);
+      d_buf = nullptr;
+      h_pin = nullptr;
+      cap = 0;
+      if (!hip_ok(hipMalloc(&d_buf, need)) ||
+          !hip_ok(hipHostMalloc((void **)&h_pin, need, hipHostMallocDefault)))
+        return false;
+      cap = need;
+    }
+    return true;
   }
-  const size_t pin = (in_bytes > out_bytes ? in_bytes : out_bytes) + 64;
-  if (pin > s.pin_cap) {
-    if (s.h_pin) (void)hipHostFree(s.h_pin);
-    s.h_pin = nullptr;
-    if (!hip_ok(hipHostMalloc((void **)&s.h_pin, pin, hipHostMallocDefault))) return false;
-    s.pin_cap = pin;
-  }
-  return true;
+};
+
+Engine &eng() {
+  static thread_local Engine e;
+  return e;
 }
 
-// upload one string and its offsets {0, len}
-bool upload(Single &s, const uint8_t *src, size_t len) {
-  if (len) memcpy(s.h_pin, src, len);
-  memset(s.h_pin + len, 0, 16);
-  if (!hip_ok(hipMemcpyAsync(s.d_in, s.h_pin, round16(len) + 16, hipMemcpyHostToDevice, s.st)))
+// H2D of the string (zero padded) and the first `meta_bytes` of meta
+bool upload(Engine &e, const Layout &l, const uint8_t *src, size_t len, size_t meta_bytes) {
+  if (len) memcpy(e.h_pin, src, len);
+  memset(e.h_pin + len, 0, l.meta - len);
+  return hip_ok(hipMemcpyAsync(e.d_buf, e.h_pin, l.meta + meta_bytes, hipMemcpyHostToDevice, e.st));
+}
+
+// the whole encode of one string: the kept output on success
+bool encode_one(Engine &e, const uint8_t *src, size_t len) {
+  e.kept = false;
+  const size_t bound = nghttp2_amd_hd_huff_encode_bound(len, 1);
+  const Layout l(len, bound);
+  if (len > 0xFFFFFFF0u || !e.reserve(l.total)) return false;
+  uint32_t *m = reinterpret_cast<uint32_t *>(e.h_pin + l.meta);
+  m[0] = 0;
+  m[1] = (uint32_t)len;
+  if (!upload(e, l, src, len, 8)) return false;
+  uint8_t *d = e.d_buf;
+  if (nghttp2_amd_hd_huff_encode_batch(d, reinterpret_cast<const uint32_t *>(d + l.meta), 1, d + l.out,
+                                       e.cap - l.out, reinterpret_cast<uint32_t *>(d + l.res), e.d_ws,
+                                       e.ws, e.st) != 0 ||
+      !hip_ok(hipMemcpyAsync(e.h_pin + l.res, d + l.res, 16 + bound, hipMemcpyDeviceToHost, e.st)) ||
+      !hip_ok(hipStreamSynchronize(e.st)))
     return false;
-  const uint32_t off[2] = {0u, (uint32_t)len};
-  return hip_ok(hipMemcpyAsync(s.d_meta, off, sizeof(off), hipMemcpyHostToDevice, s.st));
+  const uint32_t *r = reinterpret_cast<const uint32_t *>(e.h_pin + l.res);
+  if (r[1] > bound) return false;
+  e.kept_src.assign(src, src + len);
+  e.kept_out.assign(e.h_pin + l.out, e.h_pin + l.out + r[1]);
+  e.kept = true;
+  return true;
 }
 
 }  // namespace
@@ -103,39 +154,23 @@ extern "C" {
 // enclen < len, lib/nghttp2_hd.c:1011), a valid literal, never a zero
 // length prefix followed by Huffman bytes.
 size_t nghttp2_hd_huff_encode_count(const uint8_t *src, size_t len) {
-  Single &s = eng();
-  std::lock_guard<std::mutex> g(s.mu);
-  if (len > 0xFFFFFFF0u || !reserve(s, len, 64) || !upload(s, src, len)) return len;
-  uint32_t e = 0;
-  if (nghttp2_amd_hd_huff_encode_count_batch(s.d_in, s.d_meta, 1, s.d_meta + 4, s.st) != 0 ||
-      !hip_ok(hipMemcpyAsync(&e, s.d_meta + 4, 4, hipMemcpyDeviceToHost, s.st)) ||
-      !hip_ok(hipStreamSynchronize(s.st)))
-    return len;
-  return e;
+  Engine &e = eng();
+  if (!encode_one(e, src, len)) return len;
+  return e.kept_out.size();
 }
 
 int nghttp2_hd_huff_encode(nghttp2_bufs *bufs, const uint8_t *src, size_t srclen) {
-  Single &s = eng();
-  std::lock_guard<std::mutex> g(s.mu);
-  const size_t bound = nghttp2_amd_hd_huff_encode_bound(srclen, 1);
-  if (srclen > 0xFFFFFFF0u || !reserve(s, srclen, bound) || !upload(s, src, srclen))
-    return NGHTTP2_AMD_ERR_NOMEM;
-  uint32_t eoff[2] = {0, 0};
-  if (nghttp2_amd_hd_huff_encode_batch(s.d_in, s.d_meta, 1, s.d_out, s.out_cap, s.d_meta + 2,
-                                       s.d_ws, s.ws, s.st) != 0 ||
-      !hip_ok(hipMemcpyAsync(eoff, s.d_meta + 2, 8, hipMemcpyDeviceToHost, s.st)) ||
-      !hip_ok(hipStreamSynchronize(s.st)))
-    return NGHTTP2_AMD_ERR_NOMEM;
-  const size_t E = eoff[1];
-  if (E && (!hip_ok(hipMemcpyAsync(s.h_pin, s.d_out, E, hipMemcpyDeviceToHost, s.st)) ||
-            !hip_ok(hipStreamSynchronize(s.st))))
-    return NGHTTP2_AMD_ERR_NOMEM;
+  Engine &e = eng();
+  const bool hit = e.kept && e.kept_src.size() == srclen &&
+                   (srclen == 0 || memcmp(e.kept_src.data(), src, srclen) == 0);
+  if (!hit && !encode_one(e, src, srclen)) return NGHTTP2_AMD_ERR_NOMEM;
+  e.kept = false;  // one encode per count
   // Append in order with the reference's spill behaviour
   // (lib/nghttp2_hd_huffman.c:61-93): fill the current chain buffer, then
   // nghttp2_bufs_addb moves to / allocates the next one or fails with
   // NGHTTP2_ERR_BUFFER_ERROR, leaving the bytes written so far in place.
-  const uint8_t *p = s.h_pin;
-  size_t left = E;
+  const uint8_t *p = e.kept_out.data();
+  size_t left = e.kept_out.size();
   while (left) {
     nghttp2_buf *cur = &bufs->cur->buf;
     size_t avail = (size_t)(cur->end - cur->last);
@@ -164,33 +199,33 @@ void nghttp2_hd_huff_decode_context_init(nghttp2_hd_huff_decode_context *ctx) {
 
 nghttp2_ssize nghttp2_hd_huff_decode(nghttp2_hd_huff_decode_context *ctx, nghttp2_buf *buf,
                                      const uint8_t *src, size_t srclen, int fin) {
-  Single &s = eng();
-  std::lock_guard<std::mutex> g(s.mu);
+  Engine &e = eng();
   const size_t cap = srclen * 8 / 5 + 1;
-  if (srclen > 0xFFFFFFF0u || !reserve(s, srclen, cap) || !upload(s, src, srclen))
+  const Layout l(srclen, cap);
+  if (srclen > 0xFFFFFFF0u || !e.reserve(l.total)) return NGHTTP2_AMD_ERR_NOMEM;
+  uint8_t *m = e.h_pin + l.meta;
+  const uint32_t offs[4] = {0u, (uint32_t)srclen, 0u, (uint32_t)cap};
+  memcpy(m, offs, sizeof offs);
+  memcpy(m + 16, &ctx->fstate, 2);
+  m[18] = ctx->flags;
+  if (!upload(e, l, src, srclen, 20)) return NGHTTP2_AMD_ERR_NOMEM;
+  uint8_t *d = e.d_buf;
+  const uint32_t *dm = reinterpret_cast<const uint32_t *>(d + l.meta);
+  if (nghttp2_amd_hd_huff_decode_fsm_batch(d, dm, 1, d + l.out, dm + 2, reinterpret_cast<int32_t *>(d + l.res),
+                                           reinterpret_cast<uint16_t *>(d + l.res + 4), d + l.res + 6,
+                                           reinterpret_cast<const uint16_t *>(d + l.meta + 16),
+                                           d + l.meta + 18, 0, e.st) != 0 ||
+      !hip_ok(hipMemcpyAsync(e.h_pin + l.res, d + l.res, 16 + cap, hipMemcpyDeviceToHost, e.st)) ||
+      !hip_ok(hipStreamSynchronize(e.st)))
     return NGHTTP2_AMD_ERR_NOMEM;
-  // scratch in d_meta: [2..3] dst offsets, [4] status; context in d_fs/d_fl
-  const uint32_t doff[2] = {0u, (uint32_t)cap};
-  uint16_t fs = ctx->fstate;
-  uint8_t fl = ctx->flags;
-  int32_t st = 0;
-  if (!hip_ok(hipMemcpyAsync(s.d_meta + 2, doff, 8, hipMemcpyHostToDevice, s.st)) ||
-      !hip_ok(hipMemcpyAsync(s.d_fs + 4, &fs, 2, hipMemcpyHostToDevice, s.st)) ||
-      !hip_ok(hipMemcpyAsync(s.d_fl + 4, &fl, 1, hipMemcpyHostToDevice, s.st)) ||
-      nghttp2_amd_hd_huff_decode_fsm_batch(s.d_in, s.d_meta, 1, s.d_out, s.d_meta + 2,
-                                           (int32_t *)(s.d_meta + 4), s.d_fs, s.d_fl,
-                                           s.d_fs + 4, s.d_fl + 4, 0, s.st) != 0 ||
-      !hip_ok(hipMemcpyAsync(&st, s.d_meta + 4, 4, hipMemcpyDeviceToHost, s.st)) ||
-      !hip_ok(hipMemcpyAsync(&fs, s.d_fs, 2, hipMemcpyDeviceToHost, s.st)) ||
-      !hip_ok(hipMemcpyAsync(&fl, s.d_fl, 1, hipMemcpyDeviceToHost, s.st)) ||
-      !hip_ok(hipStreamSynchronize(s.st)))
-    return NGHTTP2_AMD_ERR_NOMEM;
+  int32_t st;
+  uint16_t fs;
+  memcpy(&st, e.h_pin + l.res, 4);
+  memcpy(&fs, e.h_pin + l.res + 4, 2);
+  const uint8_t fl = e.h_pin[l.res + 6];
   if (st < 0) return st;
   // decoded bytes go to buf->last (the caller guarantees srclen*8/5 bytes)
-  if (st && (!hip_ok(hipMemcpyAsync(s.h_pin, s.d_out, (size_t)st, hipMemcpyDeviceToHost, s.st)) ||
-             !hip_ok(hipStreamSynchronize(s.st))))
-    return NGHTTP2_AMD_ERR_NOMEM;
-  memcpy(buf->last, s.h_pin, (size_t)st);
+  memcpy(buf->last, e.h_pin + l.out, (size_t)st);
   buf->last += st;
   // lib/nghttp2_hd_huffman.c:135-142
   ctx->fstate = fs;

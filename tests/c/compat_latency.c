@@ -9,8 +9,13 @@
  * Usage: compat_latency <oracle.so> [strings]   -> one JSON line on stdout.
  * Strings are config-2 shaped (8..64 bytes of the pseudo-header alphabet,
  * xorshift64, fixed seed); every engine result is compared with the port's.
+ * The count and the encode after it are timed apart (the engine's count runs
+ * the whole encode and keeps it, so the encode of the same bytes takes no
+ * GPU round trip); then four host threads run the same calls concurrently
+ * (one engine per thread), every result compared with the port's.
  */
 #include <dlfcn.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,6 +40,14 @@ typedef struct {
 typedef void (*init_fn)(orc_ctx *);
 typedef long (*dec_fn)(orc_ctx *, uint8_t *, size_t *, const uint8_t *, size_t, int);
 typedef int (*oinit_fn)(void);
+
+typedef struct {
+  const uint8_t *raw, *enc;
+  const size_t *rlen, *eoff;
+  int lo, hi, bad;
+} job_t;
+
+static void *worker(void *arg);
 
 static double now(void) {
   struct timespec t;
@@ -101,7 +114,7 @@ int main(int argc, char **argv) {
   int bad = 0;
   uint8_t *ebuf = malloc(512);
   for (int pass = 0; pass < 2; ++pass) {
-    double te = 0, td = 0;
+    double te = 0, td = 0, tc = 0;
     for (int i = 0; i < n; ++i) {
       nghttp2_buf_chain ch;
       memset(&ch, 0, sizeof(ch));
@@ -115,8 +128,10 @@ int main(int argc, char **argv) {
       b.chunk_used = 1;
       double a = now();
       const size_t c = nghttp2_hd_huff_encode_count(raw + (size_t)i * 64, rlen[i]);
+      const double a2 = now();
       const int rv = nghttp2_hd_huff_encode(&b, raw + (size_t)i * 64, rlen[i]);
       te += now() - a;
+      tc += a2 - a;
       const size_t E = (size_t)(ch.buf.last - ebuf);
       if (rv != 0 || c != E || E != eoff[i + 1] - eoff[i] || memcmp(ebuf, enc + eoff[i], E) != 0) ++bad;
       nghttp2_hd_huff_decode_context ctx;
@@ -132,12 +147,65 @@ int main(int argc, char **argv) {
         ++bad;
     }
     if (pass == 1) {
+      /* four host threads, one engine each, a quarter of the strings each */
+      pthread_t th[4];
+      job_t jobs[4];
+      const double w0 = now();
+      for (int k = 0; k < 4; ++k) {
+        jobs[k].raw = raw, jobs[k].enc = enc, jobs[k].rlen = rlen, jobs[k].eoff = eoff;
+        jobs[k].lo = n * k / 4, jobs[k].hi = n * (k + 1) / 4, jobs[k].bad = 0;
+        pthread_create(&th[k], NULL, worker, &jobs[k]);
+      }
+      int tbad = 0;
+      for (int k = 0; k < 4; ++k) {
+        pthread_join(th[k], NULL);
+        tbad += jobs[k].bad;
+      }
+      const double wall4 = now() - w0;
+      bad += tbad;
       printf("{\"strings\": %d, \"raw_bytes\": %zu, \"enc_bytes\": %zu, "
-             "\"engine_encode_us_per_call\": %.2f, \"engine_decode_us_per_call\": %.2f, "
+             "\"engine_encode_us_per_call\": %.2f, \"engine_count_us_per_call\": %.2f, "
+             "\"engine_encode_after_count_us_per_call\": %.2f, \"engine_decode_us_per_call\": %.2f, "
              "\"port_encode_us_per_call\": %.4f, \"port_decode_us_per_call\": %.4f, "
+             "\"threads4_us_per_string\": %.2f, \"threads4_mismatches\": %d, "
              "\"mismatches\": %d}\n",
-             n, raw_total, total, 1e6 * te / n, 1e6 * td / n, 1e6 * port_enc, 1e6 * port_dec, bad);
+             n, raw_total, total, 1e6 * te / n, 1e6 * tc / n, 1e6 * (te - tc) / n, 1e6 * td / n,
+             1e6 * port_enc, 1e6 * port_dec, 1e6 * wall4 / n, tbad, bad);
     }
   }
   return bad ? 1 : 0;
+}
+
+/* one host thread: count + encode + decode of its strings through its own
+ * engine, each result against the port's */
+static void *worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  uint8_t ebuf[512], dec[256];
+  for (int i = j->lo; i < j->hi; ++i) {
+    const uint8_t *r = j->raw + (size_t)i * 64;
+    nghttp2_buf_chain ch;
+    memset(&ch, 0, sizeof(ch));
+    ch.buf.begin = ch.buf.pos = ch.buf.last = ch.buf.mark = ebuf;
+    ch.buf.end = ebuf + sizeof ebuf;
+    nghttp2_bufs b;
+    memset(&b, 0, sizeof(b));
+    b.head = b.cur = &ch;
+    b.chunk_length = sizeof ebuf;
+    b.max_chunk = 1;
+    b.chunk_used = 1;
+    const size_t c = nghttp2_hd_huff_encode_count(r, j->rlen[i]);
+    const int rv = nghttp2_hd_huff_encode(&b, r, j->rlen[i]);
+    const size_t E = (size_t)(ch.buf.last - ebuf);
+    if (rv != 0 || c != E || E != j->eoff[i + 1] - j->eoff[i] || memcmp(ebuf, j->enc + j->eoff[i], E) != 0)
+      ++j->bad;
+    nghttp2_hd_huff_decode_context ctx;
+    nghttp2_buf ob;
+    ob.begin = ob.pos = ob.last = ob.mark = dec;
+    ob.end = dec + sizeof dec;
+    nghttp2_hd_huff_decode_context_init(&ctx);
+    const nghttp2_ssize d = nghttp2_hd_huff_decode(&ctx, &ob, ebuf, E, 1);
+    if (d != (nghttp2_ssize)E || (size_t)(ob.last - dec) != j->rlen[i] || memcmp(dec, r, j->rlen[i]) != 0)
+      ++j->bad;
+  }
+  return NULL;
 }

@@ -310,13 +310,13 @@ def test_compat_per_call_latency(dev):
         exe = os.path.join(d, "compat_latency")
         subprocess.run(["gcc", "-O2", "-Wall", "-I", os.path.join(REPO, "include"),
                         os.path.join(REPO, "tests", "c", "compat_latency.c"), "-L" + libdir,
-                        "-lnghttp2_amd_hd", "-Wl,-rpath," + libdir, "-ldl", "-o", exe], check=True)
+                        "-lnghttp2_amd_hd", "-Wl,-rpath," + libdir, "-ldl", "-lpthread", "-o", exe], check=True)
         r = subprocess.run([exe, O.lib_path() if hasattr(O, "lib_path") else
                             os.path.join(REPO, "oracle", "_build", "libhuff_oracle.so"), "2000"],
                            capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert res["mismatches"] == 0
+    assert res["mismatches"] == 0 and res["threads4_mismatches"] == 0
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "compat_latency.json"), "w") as f:
         json.dump(res, f)
