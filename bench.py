@@ -491,12 +491,26 @@ def device_copy_gbs(torch, dev, nbytes=1 << 30, reps=10):
     return _COPY_GBS[key]
 
 
+def kernel_src_sha():
+    """sha256 (first 16 hex digits) of the kernel sources the PMC traffic
+    depends on: the traffic recorded in profiles/traffic.json is reported
+    only for the tree it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("hd_huff.hip", "hd_huff_tables.inc"):
+        with open(os.path.join(REPO, "nghttp2_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def traffic_for(cfg, n, kernel):
+    """PMC-measured HBM bytes per launch (profiles/traffic.json) when they were
+    recorded for this batch size AND these kernel sources, else None."""
     tpath = os.path.join(REPO, "profiles", "traffic.json")
     if not os.path.exists(tpath):
         return None
     tj = json.load(open(tpath)).get("config%d" % cfg, {}).get(kernel)
-    if tj and tj.get("strings") == n:
+    if tj and tj.get("strings") == n and tj.get("src_sha") == kernel_src_sha():
         return tj["hbm_bytes_per_launch"]
     return None
 

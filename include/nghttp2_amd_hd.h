@@ -121,9 +121,14 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw
  * tiles of 256 strings that fit may already be written, nothing at or past
  * dst_cap is, and no offset of the batch is valid.  A batch holding a
  * string longer than NGHTTP2_AMD_ENCODE_MAX_STRING raw bytes (its code bits
- * would not fit the kernels' 32-bit counts) is marked the same way.
+ * would not fit the kernels' 32-bit counts), or a tile of 256 consecutive
+ * strings (256 k .. 256 k + 255) whose encoded output reaches
+ * NGHTTP2_AMD_ENCODE_MAX_TILE bytes (a wave places its output bits in 32-bit
+ * positions), is marked the same way.  Header strings are far below both
+ * (nghttp2 caps a field at 64 KiB, NGHTTP2_HD_MAX_NV).
  */
 #define NGHTTP2_AMD_ENCODE_MAX_STRING (0xFFFFFFFFu / 30u)
+#define NGHTTP2_AMD_ENCODE_MAX_TILE (1u << 29)
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst, size_t dst_cap,
                                      uint32_t *dst_off, void *workspace,

@@ -399,12 +399,13 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
   if (tile_sums) {
     uint32_t tot, hi;
     // a string whose code bits would not fit the 32-bit counts, or a tile
-    // whose output might not fit 32 bits (its sum in 64 KiB units, which
-    // cannot wrap, within 256 units of 2^16: the uint32 total could have
-    // wrapped), poisons its tile's sum (0xFFFFFFFF), so this tile and every
-    // one after it overflow in k_encode
-    block_excl_scan_sum<EC_CNT_NT>(e, huge ? 0x10000u : e >> 16, red, &tot, &hi);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = hi >= 0x10000u - WG ? 0xFFFFFFFFu : tot;
+    // whose output may reach 2^29 bytes (its sum in 64 KiB units, which
+    // cannot wrap, within 256 units of 2^13: k_encode places a wave's bits
+    // in 32-bit positions), poisons its tile's sum (0xFFFFFFFF), so this tile
+    // and every one after it overflow in k_encode.  (Round 4: 64-bit bit
+    // positions in k_encode instead cost 8.7 us of 140 on config 3.)
+    block_excl_scan_sum<EC_CNT_NT>(e, huge ? 0x2000u : e >> 16, red, &tot, &hi);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = hi >= 0x2000u - WG ? 0xFFFFFFFFu : tot;
   }
 }
 
@@ -547,8 +548,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   const bool anyraw = FR && __ballot(rawl) != 0;
   // (FR: a wave of empty strings only still has its literals: one round)
   const uint32_t c_stop = FR && c_end == c0 ? c0 + 1u : c_end;
-  uint64_t x = 0;  // output bit of the round's first wave byte (relative to G0; a wave's
-                   // output may pass 2^32 bits)
+  uint32_t x = 0;  // output bit of the round's first wave byte (relative to G0; a wave's
+                   // output is below 2^32 bits: k_enc_count poisons a tile of 2^29 bytes)
   for (uint32_t cb = c0; cb < c_stop; cb += 64u) {
     const bool first = cb == c0, last_round = cb + 64u >= c_stop;
     const uint32_t base = cb << 4;
@@ -719,8 +720,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- store whole words and zero them; carry a partial last word
-    const uint64_t xe = last_round ? 8ull * (OZ - OA)
-                                   : x + (uint64_t)__builtin_amdgcn_readlane(Sinc, 63) + X0 - RA;
+    const uint32_t xe = last_round ? 8u * (OZ - OA) : x + __builtin_amdgcn_readlane(Sinc, 63) + X0 - RA;
     const uint32_t nw = (uint32_t)(((G0 + xe + 31u) >> 5) - WB);
     const uint32_t nst = last_round ? nw : (uint32_t)(((G0 + xe) >> 5) - WB);
     // words [ilo, ihi) lie inside the wave's output [OA, OZ) (<= dst_cap by
@@ -1326,12 +1326,6 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #else
 #define DD_NOOUT_ON false
 #endif
-#ifndef DD_UST40
-#define DD_UST40 true
-#endif
-#ifndef DD_UST64
-#define DD_UST64 true
-#endif
 #ifndef DD_IW40
 #define DD_IW40 16
 #endif
@@ -1770,7 +1764,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
     const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
-    uint32_t ocarry = 0;  // the partial last output word of the round before
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
     for (uint32_t r0 = 0, nv = 0; r0 < M; r0 += nv) {
@@ -1950,15 +1943,18 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- dense placement
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
-      constexpr bool kUst = IP >= 64u ? DD_UST64 : DD_UST40;
+      // ---- store: each lane stores its region straight to its output bytes
+      // with unaligned stores (gfx950 global memory takes them whole):
+      // 16-byte pieces, then the tail as 8-, 4-, 2- and 1-byte pieces.
+      // (Round 4; before, the regions were realigned to dwords by
+      // alignbyte with bytewise heads and tails, or for 64-byte items
+      // compacted in LDS and stored 16 bytes per lane: config 3 decode
+      // 249.6 -> 238.9 us, config 2 48.0 -> 43.3, config 5 130.4 -> 124.5.)
 #if defined(DD_ABL_NOOUT) || defined(DD_ABL_NOSTORE)
       if (false) {
 #else
-      if (kUst) {
-        // each lane stores its region straight to its output bytes with
-        // unaligned stores (gfx950 global memory takes them whole): 16-byte
-        // pieces, then the tail as 8-, 4-, 2- and 1-byte pieces -- no
-        // realignment and no byte-wise head
+      {
+#endif
         const uint64_t g0 = tbase + O_l;
         const bool fits = g0 + V <= dst_cap;
         const uint32_t n16 = fits ? V >> 4 : 0u;
@@ -1995,130 +1991,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         } else {  // near dst_cap: byte by byte, nothing at or past it
           for (uint32_t x = 0; x < V; ++x)
             if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
-        }
-      } else if (IP >= 64u) {
-#endif
-        // The round's bytes are the task's output [R0g, R1g): each lane moves
-        // its region into the round's global dwords [W0, W1), laid out back
-        // to back over the regions (realigned by alignbyte; the words shared
-        // by two lanes OR'ed), then the wave stores them 16 bytes per lane.
-        // The partial last word is carried into the next round (the task's
-        // last one is written whole: the next task starts 4-aligned).
-        const uint32_t Tot = __builtin_amdgcn_readlane(Tinc, 63);
-        const uint64_t R0g = tbase + run, R1g = R0g + Tot, W0 = R0g >> 2;
-        const uint64_t g0 = tbase + O_l;
-        const uint32_t h = (uint32_t)((4u - (g0 & 3u)) & 3u);  // bytes before alignment
-        const uint32_t nfull = V >= h ? (V - h) >> 2 : 0u;      // whole dwords
-        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(nfull), 63);
-        const uint32_t d0 = my_ob32[0];
-        const uint32_t vt = __builtin_amdgcn_alignbyte(my_ob32[nfull + 1u], my_ob32[nfull], h);
-        uint32_t d[di_rb(IP) / 4 + 1];
-#pragma unroll
-        for (uint32_t m0 = 0; m0 <= di_rb(IP) / 4; m0 += 4) {
-          if (m0 > mx) break;
-#pragma unroll
-          for (uint32_t j = 0; j < 4; ++j)
-            if (m0 + j <= di_rb(IP) / 4) d[m0 + j] = my_ob32[m0 + j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        lds_u32 *D = (lds_u32 *)S.ob[wv];
-        const uint32_t nwr = (uint32_t)(((R1g + 3u) >> 2) - W0);  // the round's words
-        for (uint32_t i = lane; i < nwr; i += WAVE) D[i] = 0u;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane == 0 && ocarry) atomicOr((uint32_t *)&D[0], ocarry);
-        if (V) {
-          const uint32_t wb = (uint32_t)((g0 >> 2) - W0);
-          if (h) {  // my first bytes share a word with the lanes before
-            const uint32_t nh = min(h, V);
-            const uint32_t mk = (nh == 4u ? 0xFFFFFFFFu : (1u << (8u * nh)) - 1u) << (8u * (4u - h));
-            atomicOr((uint32_t *)&D[wb], (d0 << (8u * (4u - h))) & mk);
-          }
-          const uint32_t wf = wb + (h ? 1u : 0u);
-#pragma unroll
-          for (uint32_t m0 = 0; m0 < di_rb(IP) / 4; m0 += 4) {
-            if (m0 >= mx) break;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-              const uint32_t m = m0 + j;
-              if (m < di_rb(IP) / 4 && m < nfull) D[wf + m] = __builtin_amdgcn_alignbyte(d[m + 1u], d[m], h);
-            }
-          }
-          const uint32_t xt = h + 4u * nfull;
-          if (V > xt) atomicOr((uint32_t *)&D[wf + nfull], vt & ((1u << (8u * (V - xt))) - 1u));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const bool lastr = r0 + nv >= M;
-        const uint32_t nst = lastr ? nwr : (uint32_t)((R1g >> 2) - W0);
-        for (uint32_t i4 = 4u * lane; i4 < nst; i4 += 4u * WAVE) {
-          const uint64_t gq = 4ull * (W0 + i4);
-          if (i4 + 4u <= nst && gq + 16u <= dst_cap) {
-            const u32x4 v = *(const lds_u32x4 *)(D + i4);
-            *reinterpret_cast<uint4 *>(dst + gq) = make_uint4(v.x, v.y, v.z, v.w);
-          } else {
-            for (uint32_t u = 0; u < 4u && i4 + u < nst; ++u) {
-              const uint32_t v = D[i4 + u];
-              const uint64_t q = gq + 4u * u;
-              if (q + 4u <= dst_cap) {
-                *reinterpret_cast<uint32_t *>(dst + q) = v;
-              } else {
-                for (uint32_t y = 0; y < 4u; ++y)
-                  if (q + y < dst_cap) dst[q + y] = (uint8_t)(v >> (8u * y));
-              }
-            }
-          }
-        }
-        ocarry = (!lastr && nst < nwr) ? __builtin_amdgcn_readfirstlane(D[nst]) : 0u;
-      } else if (!DD_NOOUT_ON) {
-        // dwords realigned to the output (alignbyte) for as many dwords as
-        // the wave's longest region, four per step; the bytes before the
-        // first aligned dword and after the last one stored singly
-        const uint64_t g0 = tbase + O_l;
-        const uint32_t h = (uint32_t)((4u - (g0 & 3u)) & 3u);  // bytes before alignment
-        const bool fits = g0 + V <= dst_cap;
-        const uint32_t nfull = V >= h ? (V - h) >> 2 : 0u;      // whole dwords
-        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(fits ? nfull : 0u), 63);
-        uint32_t prev = my_ob32[0];
-        const uint32_t d0 = prev;
-#pragma unroll
-        for (uint32_t m0 = 0; m0 < di_rb(IP) / 4; m0 += 4) {
-          if (m0 >= mx) break;
-          uint32_t c[4];
-#pragma unroll
-          for (uint32_t j = 0; j < 4; ++j) c[j] = m0 + j < di_rb(IP) / 4 ? my_ob32[m0 + j + 1u] : 0u;
-          uint32_t v[4];
-#pragma unroll
-          for (uint32_t j = 0; j < 4; ++j) v[j] = __builtin_amdgcn_alignbyte(c[j], j ? c[j - 1] : prev, h);
-          if (m0 + 4u <= nfull && fits) {
-            // four whole dwords as one (dword-aligned) 16-byte store
-            dd_st16(reinterpret_cast<uint4 *>(dst + g0 + h + 4u * m0), make_uint4(v[0], v[1], v[2], v[3]));
-          } else {
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j)
-              if (m0 + j < nfull && fits) *reinterpret_cast<uint32_t *>(dst + g0 + h + 4u * (m0 + j)) = v[j];
-          }
-          prev = c[3];
-        }
-        if (V) {
-          const uint32_t vt = __builtin_amdgcn_alignbyte(my_ob32[nfull + 1u], my_ob32[nfull], h);
-          const uint32_t nh = min(h, V);
-          const uint32_t xt = h + 4u * nfull, ntl = V > xt ? V - xt : 0u;
-          {
-#pragma unroll
-            for (uint32_t x = 0; x < 3u; ++x) {
-              if (x < nh && fits) dst[g0 + x] = (uint8_t)(d0 >> (8u * x));
-              if (x < ntl && fits) dst[g0 + xt + x] = (uint8_t)(vt >> (8u * x));
-            }
-          }
-          if (!fits) {  // near dst_cap: byte by byte, nothing at or past it
-            for (uint32_t x = 0; x < V; ++x)
-              if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
-          }
         }
       }
       run += __builtin_amdgcn_readlane(Tinc, 63);

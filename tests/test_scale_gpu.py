@@ -240,32 +240,37 @@ def test_encode_string_past_max_marks_overflow(codec, dev):
     torch.cuda.empty_cache()
 
 
-def test_encode_wave_output_past_2_32_bits(codec, dev):
-    """Six 30 MB strings of 0xFF (26-bit codes) in one wave: each far below
-    NGHTTP2_AMD_ENCODE_MAX_STRING, the batch 585 MB encoded (it fits the
-    offsets), but one wave writes 4.7e9 bits -- past a 32-bit bit position.
-    Every byte and offset equals the oracle's; then the same batch with a
-    pool 1 MB short of its total overflows without a byte past dst_cap."""
+def test_encode_wave_output_near_2_32_bits(codec, dev):
+    """Four 30 MB strings of 0xFF (26-bit codes) in one wave: each far below
+    NGHTTP2_AMD_ENCODE_MAX_STRING, one wave writes 3.3e9 bits (390 MB, under
+    the 2^29-byte tile limit): every byte and offset equals the oracle's.
+    Six of them (585 MB in one 256-string tile, 4.7e9 bits, past 32-bit bit
+    positions) mark the batch overflowed, even with a pool that holds them,
+    and no byte is written past dst_cap."""
     import torch
-    L, n = 30 << 20, 6
-    raw = L * n
-    off = (np.arange(n + 1, dtype=np.int64) * L).astype(np.uint32)
+    L = 30 << 20
     one, _ = O.encode_batch(np.full(L + 16, 0xFF, np.uint8), np.array([0, L], np.uint32))
     E1 = len(one)
-    assert E1 == (26 * L + 7) // 8 and 8 * E1 * n > (1 << 32)
-    src = torch.full((raw + 32,), 0xFF, dtype=torch.uint8, device=dev)
-    enc, eoff = codec.encode(src, to_dev(off, dev), raw_bytes=raw)
+    assert E1 == (26 * L + 7) // 8
+    src = torch.full((6 * L + 32,), 0xFF, dtype=torch.uint8, device=dev)
+    ref = torch.from_numpy(np.frombuffer(bytes(one), np.uint8).copy()).to(dev)
+    n = 4
+    off = (np.arange(n + 1, dtype=np.int64) * L).astype(np.uint32)
+    assert 8 * E1 * n > (3 << 30) and E1 * n < (1 << 29)
+    enc, eoff = codec.encode(src, to_dev(off, dev), raw_bytes=n * L)
     torch.cuda.synchronize()
     eo = _u32(eoff).astype(np.int64)
     assert np.array_equal(eo, np.arange(n + 1) * E1), "offsets"
-    ref = torch.from_numpy(np.frombuffer(bytes(one), np.uint8).copy()).to(dev)
     for i in range(n):
         assert torch.equal(enc[i * E1:(i + 1) * E1], ref), "string %d" % i
     del enc
-    cap = n * E1 - (1 << 20)
-    dst = torch.full((n * E1 + 4096,), 0xAB, dtype=torch.uint8, device=dev)
+    n = 6
+    off = (np.arange(n + 1, dtype=np.int64) * L).astype(np.uint32)
+    assert E1 * n >= (1 << 29)
+    cap = codec.encode_bound(n * L, n)
+    dst = torch.full((cap + 4096,), 0xAB, dtype=torch.uint8, device=dev)
     eoff2 = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    codec.encode(src, to_dev(off, dev), raw_bytes=raw, dst=dst[:cap], dst_off=eoff2)
+    codec.encode(src, to_dev(off, dev), raw_bytes=n * L, dst=dst[:cap], dst_off=eoff2)
     torch.cuda.synchronize()
     assert _u32(eoff2)[-1] == 0xFFFFFFFF, "overflow mark"
     assert bool((dst[cap:] == 0xAB).all()), "a byte past dst_cap was written"

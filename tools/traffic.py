@@ -30,6 +30,9 @@ def per_launch(d, counter):
 
 
 def main():
+    sys.path.insert(0, ROOT)
+    from bench import kernel_src_sha
+    src_sha = kernel_src_sha()  # the tree the counters were measured on (bench.py checks it)
     out_path = os.path.join(ROOT, "profiles", "traffic.json")
     res = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for cfg, strings in ((2, 1 << 20), (3, 1 << 20), (5, 1 << 20)):
@@ -44,6 +47,7 @@ def main():
             if k in fetch and k in write:
                 rd, wr = 2.0 * fetch[k] * 1024, write[k] * 1024
                 ent[k] = {"strings": strings, "read_bytes": int(rd), "write_bytes": int(wr),
+                          "src_sha": src_sha,
                           "hbm_bytes_per_launch": int(rd + wr),
                           "source": "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                     "FETCH x2 per MI355X_MICROARCH.md)" % os.path.relpath(d, ROOT)}
