@@ -611,7 +611,11 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
         uint32_t c[4], l[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+#ifndef DE_ABL_NOLUT
           const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(4 * m + u));
+#else
+          const uint2 cj = make_uint2(EC_B8(4 * m + u) << 21, 5u + ((EC_B8(4 * m + u) >> 3) & 1u));
+#endif
           c[u] = cj.x;
           l[u] = cj.y + ((pd[m] >> (8 * u)) & 0xFFu);
         }
@@ -670,7 +674,11 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
         uint32_t b = ib0;
 #pragma unroll
         for (int m = 0; m < (FR ? 8 : 4); ++m) {
+#ifndef DE_ABL_NOOR
           ec_or3(img, b, qh[m], qo[m]);
+#else
+          if (qh[m] == 0x12345u) img[b >> 5] = qo[m];  // (keep the quads live)
+#endif
           b += ql[m];
         }
       } else {  // a code of <= 37 bits, MSB-aligned in 64; one dword at a time
@@ -1400,7 +1408,42 @@ struct LdsPtrSink {
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
   __device__ __forceinline__ void flush() {}
 };
+// Output gathered in a register word and written one dword per step (pair):
+// w = the step's 1-4 bytes, appended to the pending bytes `acc` (nb bits);
+// the dword at q is (re)written each step with what it holds so far and q
+// advances when it is full.  One ds_write_b32 instead of two ds_write_b8 per
+// entry: ~10 more VALU per pair, 12 LDS-store cycles less.
+struct AccSink {
+  lds_u32 *q, *base;
+  uint32_t acc, nb;
+  __device__ __forceinline__ AccSink(lds_u8 *b) : q((lds_u32 *)b), base((lds_u32 *)b), acc(0), nb(0) {}
+  __device__ __forceinline__ uint32_t count() const { return 4u * (uint32_t)(q - base) + (nb >> 3); }
+  __device__ __forceinline__ void add(uint32_t w, uint32_t cw) {
+    const uint32_t lo = acc | (w << nb);
+    const uint32_t hi = __builtin_amdgcn_alignbit(w, 0u, 32u - nb);  // (nb = 0: 0)
+    *q = lo;
+    const uint32_t t = nb + cw;
+    const bool full = t >= 32u;
+    q += full ? 1 : 0;
+    acc = full ? hi : lo;
+    nb = t & 31u;
+  }
+  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
+    add(__builtin_amdgcn_perm(0u, v, 0x0C0C0200u), c8);
+  }
+  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
+    const uint32_t c1 = E_CNT8(e1);
+    add(__builtin_amdgcn_perm(0u, e1, 0x0C0C0200u) | (__builtin_amdgcn_perm(0u, e2, 0x0C0C0200u) << c1),
+        c1 + E_CNT8(e2));
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
+  __device__ __forceinline__ void flush() {}
+};
+#ifdef DD_ACC2
+typedef AccSink DISink;
+#else
 typedef LdsPtrSink DISink;
+#endif
 
 // the item decoder's 16-byte input loads and output stores
 __device__ __forceinline__ uint4 dd_ld16(const uint4 *p) { return *p; }
@@ -1640,6 +1683,30 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
   }
 }
 
+#ifdef DD_STAMPS
+// Diagnostic build only (tools/diag/stamps.py): per-phase shader-clock
+// sums of the item decoder's waves, read back by nghttp2_amd_hd__stamps.
+__device__ unsigned long long dd_stamps[16];
+#define DD_STAMP_INIT() uint64_t st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_prev_ = __builtin_amdgcn_s_memtime()
+#define DD_STAMP(k)                                        \
+  do {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+    st_acc_[k] += t_ - st_prev_;                           \
+    st_prev_ = t_;                                         \
+  } while (0)
+#define DD_STAMP_COUNT(k) (st_acc_[k] += 1)
+#define DD_STAMP_FLUSH()                                                   \
+  do {                                                                     \
+    if (lane == 0)                                                         \
+      for (int k_ = 0; k_ < 10; ++k_) atomicAdd(&dd_stamps[k_], (unsigned long long)st_acc_[k_]); \
+  } while (0)
+#else
+#define DD_STAMP_INIT() do {} while (0)
+#define DD_STAMP(k) do {} while (0)
+#define DD_STAMP_COUNT(k) do {} while (0)
+#define DD_STAMP_FLUSH() do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Dense decode by items (decode_batch_auto): a string of <= DD_P encoded
 // bytes is one item, a longer one is cut into items of DD_P bytes; a wave
@@ -1673,6 +1740,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   if (threadIdx.x == 0) S.claimed = 0u;
   stage_dec_tables(S.T, (WAVE * IW));  // the kernel's only workgroup barrier
   const uint32_t off0 = off[0];
+  DD_STAMP_INIT();
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
   // this workgroup's tasks: with 40-byte pieces (long values, whose tasks
   // differ several-fold in work) a contiguous range balanced by weight
@@ -1766,7 +1834,9 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
+    DD_STAMP(0);  // task setup
     for (uint32_t r0 = 0, nv = 0; r0 < M; r0 += nv) {
+      DD_STAMP_COUNT(8);
       nv = min(M - r0, (uint32_t)WAVE);  // (budgeted rounds: cut below)
       const uint32_t q = r0 + lane;
       // this lane's item: its string i = the last one with X_i <= q; every
@@ -1807,6 +1877,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const bool valid = lane < nv;
       const bool last = e == b;
       const bool spec = valid && k > 0;
+      DD_STAMP(1);  // item map
       // ---- stage [first item (- OV), last item's end + 8)
       uint32_t IB, nchunk;
       round_range(R0, A, Z, IB, nchunk);
@@ -1838,6 +1909,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             if (lane + WAVE * u < nchunk) pf[u] = dd_ld16(g + lane + WAVE * u);
         }
         stage_pf(nchunk);
+        DD_STAMP(9);  // staging: the wait for the prefetched chunks and their LDS writes
         // prefetch the next round: of this task, else the next task's first
         pf_IB = 0xFFFFFFFFu;
         uint32_t IBn = 0, ncn = 0;
@@ -1864,6 +1936,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
       const uint32_t bstop = last ? bend : 8u * (e - IBX);
       DISink sk(my_ob);
+      DD_STAMP(2);  // staging
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
@@ -1874,6 +1947,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         entry = bp;
         dead = rw.failed;
       }
+      DD_STAMP(3);  // warm-up
       // ---- the item's symbols
       uint32_t bp = entry;
       DDRun rr;
@@ -1928,6 +2002,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           my_entry = pred;
         }
       }
+      DD_STAMP(4);  // decode + verify
       // ---- string symbol counts: segmented scan (heads: first items)
       // (the plain inclusive scan of the lanes' byte counts, less its value
       // before the lane's last head; no head yet: plus the carried count)
@@ -1943,6 +2018,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- dense placement
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
+      DD_STAMP(5);  // scans + finish
       // ---- store: each lane stores its region straight to its output bytes
       // with unaligned stores (gfx950 global memory takes them whole):
       // 16-byte pieces, then the tail as 8-, 4-, 2- and 1-byte pieces.
@@ -1959,7 +2035,26 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         const bool fits = g0 + V <= dst_cap;
         const uint32_t n16 = fits ? V >> 4 : 0u;
         const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(n16), 63);
+#if defined(DD_ABL_COALST)
+        {  // ablation: the round's bytes stored contiguously, 16 B per lane (garbage order)
+          const uint32_t Tot = __builtin_amdgcn_readlane(Tinc, 63);
+          const uint64_t G = (tbase + run) & ~15ull;
+          for (uint32_t c = lane; 16u * c < Tot + 16u; c += WAVE) {
+            u32x4 v;
+            v.x = my_ob32[(4u * c) & 15u];
+            v.y = my_ob32[(4u * c + 1u) & 15u];
+            v.z = my_ob32[(4u * c + 2u) & 15u];
+            v.w = my_ob32[(4u * c + 3u) & 15u];
+            if (G + 16u * c + 16u <= dst_cap) *(u32x4 *)(dst + G + 16u * c) = v;
+          }
+        }
+        if (false) {
+#endif
+#ifdef DD_ABL_ALIGNST
+        uint8_t *o = dst + (g0 & ~15ull);
+#else
         uint8_t *o = dst + g0;
+#endif
 #pragma unroll
         for (uint32_t m = 0; m < (di_rb(IP) + 15u) / 16u; ++m) {
           if (m >= mx) break;
@@ -1992,7 +2087,11 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           for (uint32_t x = 0; x < V; ++x)
             if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
         }
+#if defined(DD_ABL_COALST)
+        }
+#endif
       }
+      DD_STAMP(6);  // store
       run += __builtin_amdgcn_readlane(Tinc, 63);
       R0 = __builtin_amdgcn_readlane(e, nv - 1u);
       carry_exit = __builtin_amdgcn_readlane(last ? DD_NONE : my_exit, nv - 1u);
@@ -2009,8 +2108,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    DD_STAMP(7);  // round tails + epilogue
     task = next_task;
   }
+  DD_STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -2307,6 +2408,18 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
                      fstate, flags);
   return hip_rv(hipGetLastError());
 }
+
+#ifdef DD_STAMPS
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__stamps(uint64_t *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dd_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
+    return NGHTTP2_AMD_ERR_FATAL;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(dd_stamps), z, sizeof z) != hipSuccess) return NGHTTP2_AMD_ERR_FATAL;
+  }
+  return 0;
+}
+#endif
 
 int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint64_t enc_bytes, uint8_t *dst,

@@ -18,6 +18,7 @@ Tensors are torch CUDA (HIP) tensors: uint8 pools, int32 tensors holding
 uint32 offsets.  Errors follow nghttp2: negative nghttp2_error codes raise
 RuntimeError; per-string decode status is an int32 tensor.
 """
+import collections
 import ctypes
 import os
 
@@ -132,12 +133,18 @@ class HuffmanBatchCodec:
     stream run in issue order, as any work on a stream does.
     """
 
+    _SCRATCH_KEEP = 16  # per-stream workspaces kept (two kinds per stream)
+
     def __init__(self, device=None):
         import torch
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
         self.L = lib()
-        self._scratch = {}  # (stream handle, kind) -> uint8 tensor allocated on that stream
+        # (stream handle, kind) -> uint8 tensor allocated on that stream; the
+        # least recently used entries past _SCRATCH_KEEP are dropped, so
+        # short-lived streams do not pin device workspace (a dropped block
+        # returns to the caching allocator on the stream it was allocated on)
+        self._scratch = collections.OrderedDict()
 
     def _on(self, stream):
         return stream if stream is not None else self.torch.cuda.current_stream(self.device)
@@ -146,6 +153,8 @@ class HuffmanBatchCodec:
         s = self._on(stream)
         key = (s.cuda_stream, kind)
         t = self._scratch.get(key)
+        if t is not None:
+            self._scratch.move_to_end(key)
         if t is None or t.numel() < need:
             # Uninitialised on purpose: the kernels write every scratch word
             # they read (a zero fill would be one more kernel).  Allocated
@@ -154,6 +163,8 @@ class HuffmanBatchCodec:
             with self.torch.cuda.stream(s):
                 t = self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
             self._scratch[key] = t
+            while len(self._scratch) > self._SCRATCH_KEEP:
+                self._scratch.popitem(last=False)
         return t
 
     def _empty(self, n, dtype, stream):
