@@ -1334,6 +1334,15 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #else
 #define DD_NOOUT_ON false
 #endif
+#ifndef DD_IW64
+#define DD_IW64 16
+#endif
+#ifndef DD_BI64
+#define DD_BI64 2304u
+#endif
+#ifndef DD_BI40
+#define DD_BI40 0u
+#endif
 #ifndef DD_IW40
 #define DD_IW40 16
 #endif
@@ -2263,9 +2272,9 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
   if (enc_bytes <= 48ull * n)
-    launch_decode_items<64u, 16, 13, 2304u>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<64u, DD_IW64, 13, DD_BI64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
-    launch_decode_items<40u, DD_IW40, 13, 0u, DD_SK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<40u, DD_IW40, 13, DD_BI40, DD_SK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
 }
 
