@@ -71,6 +71,9 @@ def parse():
                     help="also time the pinned-host H2D+D2H round trip")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (auto: nccl = RCCL)")
+    ap.add_argument("--dump-dir", default=None,
+                    help="(tests) each rank writes its shard bounds, encoded pool, offsets and "
+                         "decode status there after the warm-up, for an outside check")
     return ap.parse_args()
 
 
@@ -326,6 +329,11 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     assert np.array_equal(st, raw_len), "decode(encode(x)) length mismatch"
     assert int(P0.enc_off[-1].item()) & 0xFFFFFFFF == enc_total
     verify_roundtrip(P0.dec, P0.dec_off.cpu().numpy().view(np.uint32), pool, off)
+    if args.dump_dir:
+        rk = int(os.environ.get("RANK", "0"))
+        np.savez(os.path.join(args.dump_dir, "rank%d.npz" % rk), data=np.array(data),
+                 enc=P0.enc[:enc_total].cpu().numpy(),
+                 enc_off=P0.enc_off.cpu().numpy().view(np.uint32), status=st)
 
     progress("config %d: round trip checked, timing" % cfg)
     # per-kernel timing (roofline): K plain steps with events on the stream

@@ -423,7 +423,9 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
+#ifndef EC_WPE
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
+#endif
 #define EC_M 16u                    // image margin (words): >= 15 bytes x 30 bits
 #define EC_RW (EC_M + 1024u + 32u)  // + 1 KB at <= 32 bits a byte + carry + bytes past Z
 // FR: + the wave's literal prefixes and pads (64 x (6 x 8 + 7) bits)

@@ -286,23 +286,38 @@ def _free_port():
     return p
 
 
-def test_bench_two_ranks_gloo_one_gpu(dev):
+def test_bench_two_ranks_gloo_one_gpu(dev, tmp_path):
     """bench.py's N > 1 path (init, byte-balanced config-4 shard per rank,
     barrier, max-over-ranks time, summed bytes) as 2 ranks on the one GPU,
-    collectives over gloo."""
+    collectives over gloo; each rank's encoded shard (bytes and offsets) is
+    then checked against the oracle's encode of the same shard, and its
+    decode status against the raw lengths."""
+    from nghttp2_amd import shard as S
+    from nghttp2_amd import workloads as W
+    total = 1 << 21
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--config", "4",
-           "--strings", str(1 << 21), "--steps", "3", "--warmup", "1", "--streams", "1",
-           "--no-cpu-baseline"]
+           "--strings", str(total), "--steps", "3", "--warmup", "1", "--streams", "1",
+           "--no-cpu-baseline", "--dump-dir", str(tmp_path)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["value"] > 0
     # the two shards cover the set: 2 * strings_per_gpu is about 2M
-    assert abs(2 * out["config"]["strings_per_gpu"] - (1 << 21)) < 4096
+    assert abs(2 * out["config"]["strings_per_gpu"] - total) < 4096
+    lengths = W.mixed_lengths(total)
+    all_off = np.zeros(total + 1, dtype=np.int64)
+    np.cumsum(lengths, out=all_off[1:])
+    for rk, (s0, s1) in enumerate(S.byte_balanced_bounds(all_off, 2)):
+        d = np.load(str(tmp_path / ("rank%d.npz" % rk)))
+        pool, off = W.gen_mixed_range(lengths, s0, s1)
+        renc, reoff = O.encode_batch(pool, off, nthreads=8)
+        assert np.array_equal(d["enc_off"], reoff), "rank %d: encoded offsets" % rk
+        assert np.array_equal(d["enc"], renc[:int(reoff[-1])]), "rank %d: encoded bytes" % rk
+        assert np.array_equal(d["status"], np.diff(off.astype(np.int64))), "rank %d: status" % rk
 
 
 def test_compat_per_call_latency(dev):
