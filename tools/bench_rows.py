@@ -110,8 +110,8 @@ def bench_names(steps=50, long_frac=0.02):
 
 
 def make_blocks(nconn, per_conn, fields_per_block, seed=7):
-    """Header blocks as a deflater would send them: repeated names indexed,
-    values as literals with incremental indexing (Huffman when shorter)."""
+    """Header blocks of two indexed static fields and `fields_per_block`
+    literal fields without indexing, new name (Huffman when shorter)."""
     from oracle import oracle as O
     from nghttp2_amd import workloads as W
     rng = np.random.Generator(np.random.PCG64(seed))
