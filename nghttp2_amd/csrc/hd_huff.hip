@@ -274,7 +274,9 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 }
 
 #define ENC_WAVES 4                  // waves per encode workgroup (tile = 256 strings)
+#ifndef EC_CNT_PFD
 #define EC_CNT_PFD 2  // k_enc_count: rounds of chunks in flight per wave (4: no faster)
+#endif
 
 // bytes of the 7-bit-prefix integer n (count_encoded_length(n, 7))
 __device__ __forceinline__ uint32_t prefix7_len(uint32_t n) {
@@ -353,10 +355,18 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
       q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
       if (cb + 64u * EC_CNT_PFD + lane < c_end)
         q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
+#if defined(DE_ABL_CNT_STREAM)  // diag: the loads alone (wrong counts; timing only)
+      Rc += wd[0] ^ wd[1] ^ wd[2] ^ wd[3];
+      continue;
+#endif
       uint32_t run = 0, pk[8];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
+#if defined(DE_ABL_CNT_NOLUT)  // diag: no length lookups (wrong counts; timing only)
+        const uint32_t L = (wd[j >> 2] >> (8 * (j & 3))) & 0x7u;
+#else
         const uint32_t L = lenT[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+#endif
         if (j & 1) pk[j >> 1] |= run << 16; else pk[j >> 1] = run;
         run += L;
       }

@@ -23,7 +23,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <deque>
 #include <unordered_map>
 #include <mutex>
 #include <new>
@@ -59,14 +58,85 @@ const char *const kStatic[kStaticLen][2] = {
     {"set-cookie", ""}, {"strict-transport-security", ""}, {"transfer-encoding", ""},
     {"user-agent", ""}, {"vary", ""}, {"via", ""}, {"www-authenticate", ""}};
 
-struct Entry {
-  std::string name, value;
+// The dynamic table (lib/nghttp2_hd.c hd_ringbuf + nghttp2_hd_entry, restated
+// without a heap object per entry): entry descriptors in a power-of-two ring,
+// the entries' name/value bytes in one byte ring, each entry contiguous (an
+// entry that would cross the ring's end starts at 0 and the tail is skipped).
+// Insertion and eviction allocate nothing once the rings have grown to the
+// connection's working size; a ring that cannot place an entry is compacted
+// into one twice as large.
+struct DynTable {
+  struct Ent {
+    size_t off;
+    uint32_t nl, vl;
+  };
+  std::vector<Ent> ents;   // ring, capacity a power of two
+  size_t e_first = 0;      // oldest entry
+  size_t count = 0;
+  std::vector<uint8_t> buf;  // byte ring
+
+  const Ent &newest(size_t k) const {  // k = 0: the most recent (dynamic index 62)
+    return ents[(e_first + count - 1 - k) & (ents.size() - 1)];
+  }
+  const uint8_t *name(const Ent &e) const { return buf.data() + e.off; }
+  const uint8_t *value(const Ent &e) const { return buf.data() + e.off + e.nl; }
+  size_t bytes(const Ent &e) const { return (size_t)e.nl + e.vl; }
+  void pop_oldest() {
+    e_first = (e_first + 1) & (ents.size() - 1);
+    --count;
+  }
+  // offset for s contiguous bytes, or SIZE_MAX.  Occupied: [head, tail)
+  // unwrapped, or [head, cap) + [0, tail) once the newest entry sits before
+  // the oldest; placements keep one byte free before head so the two stay
+  // distinguishable.
+  size_t place(size_t s) const {
+    const size_t cap = buf.size();
+    if (count == 0) return s <= cap ? 0 : SIZE_MAX;
+    const Ent &o = ents[e_first], &w = newest(0);
+    const size_t head = o.off, tail = w.off + bytes(w);
+    if (w.off >= head) {  // unwrapped
+      if (cap - tail >= s) return tail;
+      return s < head ? 0 : SIZE_MAX;
+    }
+    return tail + s < head ? tail : SIZE_MAX;
+  }
+  void grow(size_t need) {  // compact the entries, oldest first, into a larger ring
+    size_t live = 0;
+    for (size_t k = 0; k < count; ++k) live += bytes(newest(k));
+    std::vector<uint8_t> nb(std::max<size_t>(std::max<size_t>(2 * buf.size(), 2 * (live + need) + 2), 256));
+    size_t at = 0;
+    for (size_t k = count; k-- > 0;) {
+      Ent &e = ents[(e_first + count - 1 - k) & (ents.size() - 1)];
+      if (bytes(e)) memcpy(nb.data() + at, buf.data() + e.off, bytes(e));
+      e.off = at;
+      at += bytes(e);
+    }
+    buf.swap(nb);
+  }
+  // n / v must not point into this table (the caller passes copies)
+  void push(const uint8_t *n, size_t nl, const uint8_t *v, size_t vl) {
+    if (count == ents.size()) {  // grow the descriptor ring, oldest first
+      std::vector<Ent> ne(ents.empty() ? 16 : 2 * ents.size());
+      for (size_t k = 0; k < count; ++k) ne[k] = ents[(e_first + k) & (ents.size() - 1)];
+      ents.swap(ne);
+      e_first = 0;
+    }
+    size_t at = place(nl + vl);
+    if (at == SIZE_MAX) {
+      grow(nl + vl);
+      at = place(nl + vl);
+    }
+    if (nl) memcpy(buf.data() + at, n, nl);
+    if (vl) memcpy(buf.data() + at + nl, v, vl);
+    ents[(e_first + count) & (ents.size() - 1)] = Ent{at, (uint32_t)nl, (uint32_t)vl};
+    ++count;
+  }
 };
 
 }  // namespace
 
 struct nghttp2_amd_hd_inflater {
-  std::deque<Entry> table;  // front = most recent (dynamic index 62)
+  DynTable table;
   size_t bufsize = 0;
   size_t bufsize_max = kDefaultTable;           // ctx.hd_table_bufsize_max
   size_t settings_max = kDefaultTable;          // settings_hd_table_bufsize_max
@@ -74,25 +144,25 @@ struct nghttp2_amd_hd_inflater {
   bool expect_size = false;                     // NGHTTP2_HD_STATE_EXPECT_TABLE_SIZE
   bool bad = false;                             // ctx.bad
 
-  void shrink() {  // hd_context_shrink_table_size
-    while (bufsize > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+  void evict_oldest() {
+    bufsize -= table.bytes(table.ents[table.e_first]) + kEntryOverhead;
+    table.pop_oldest();
   }
-  // add_hd_table_incremental: e is built (copied) before any eviction, so a
-  // name taken from an entry that gets evicted stays valid
-  void add(Entry &&e) {
-    const size_t room = e.name.size() + e.value.size() + kEntryOverhead;
-    while (bufsize + room > bufsize_max && !table.empty()) {
-      bufsize -= table.back().name.size() + table.back().value.size() + kEntryOverhead;
-      table.pop_back();
-    }
+  void shrink() {  // hd_context_shrink_table_size
+    while (bufsize > bufsize_max && table.count) evict_oldest();
+  }
+  // add_hd_table_incremental (:1130-1195): evict until the entry fits, then
+  // insert it unless it is larger than the whole table.  n / v are copies
+  // outside the table (the caller's emitted field), so a name taken from an
+  // entry that this insertion evicts stays valid, as in the reference.
+  void add(const uint8_t *n, size_t nl, const uint8_t *v, size_t vl) {
+    const size_t room = nl + vl + kEntryOverhead;
+    while (bufsize + room > bufsize_max && table.count) evict_oldest();
     if (room > bufsize_max) return;
-    table.push_front(std::move(e));
+    table.push(n, nl, v, vl);
     bufsize += room;
   }
-  size_t max_index() const { return table.size() + kStaticLen; }  // get_max_index
+  size_t max_index() const { return table.count + kStaticLen; }  // get_max_index
 };
 
 namespace {
@@ -141,6 +211,17 @@ struct Block {
   bool parse_ok = true;
 };
 
+// One block's emitted fields: name\0value\0 runs in `bytes`.
+struct Rec {
+  uint32_t name_off, name_len, value_off, value_len;
+  uint8_t flags;
+};
+struct BlockOut {
+  std::vector<Rec> recs;
+  std::string bytes;
+  int32_t status = 0;
+};
+
 struct Engine {
   std::mutex mu;
   uint8_t *h_pool = nullptr;  // pinned: Huffman literals in, decoded out
@@ -151,6 +232,7 @@ struct Engine {
   uint32_t *d_off = nullptr, *d_slot = nullptr;
   int32_t *d_st = nullptr;
   size_t din_cap = 0, dout_cap = 0, dn_cap = 0;
+  std::vector<BlockOut> outs;
 };
 Engine &engine() {
   static Engine e;
@@ -246,17 +328,6 @@ struct LitSrc {
   }
 };
 
-// One block's emitted fields: name\0value\0 runs in `bytes`.
-struct Rec {
-  uint32_t name_off, name_len, value_off, value_len;
-  uint8_t flags;
-};
-struct BlockOut {
-  std::vector<Rec> recs;
-  std::string bytes;
-  int32_t status = 0;
-};
-
 size_t static_len(uint32_t idx, int which) {
   static size_t lens[kStaticLen][2];
   static bool init = [] {
@@ -297,11 +368,11 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
       *v = kStatic[idx][1];
       *vl = static_len(idx, 1);
     } else {
-      const Entry &e = inf->table[idx - kStaticLen];
-      *n = e.name.data();
-      *nl = e.name.size();
-      *v = e.value.data();
-      *vl = e.value.size();
+      const DynTable::Ent &e = inf->table.newest(idx - kStaticLen);
+      *n = (const char *)inf->table.name(e);
+      *nl = e.nl;
+      *v = (const char *)inf->table.value(e);
+      *vl = e.vl;
     }
   };
   bool ok = !inf->bad;
@@ -354,12 +425,11 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
       break;
     }
     const uint8_t flags = op.no_index ? 1u : 0u;  // NGHTTP2_NV_FLAG_NO_INDEX
-    if (op.index_required) {
-      Entry e{std::string(n, nl), std::string(v, vl)};
-      emit(e.name.data(), e.name.size(), e.value.data(), e.value.size(), flags);
-      inf->add(std::move(e));
-    } else {
-      emit(n, nl, v, vl, flags);
+    emit(n, nl, v, vl, flags);
+    if (op.index_required) {  // the table copies the field just emitted
+      const Rec &r = out.recs.back();
+      const uint8_t *ob = (const uint8_t *)out.bytes.data();
+      inf->add(ob + r.name_off, nl, ob + r.value_off, vl);
     }
   }
   // truncated or malformed wire after the parsed representations; and a
@@ -414,11 +484,11 @@ int nghttp2_amd_hd_inflate_get_table_entry(nghttp2_amd_hd_inflater *inf, size_t 
     *value = (const uint8_t *)kStatic[idx][1];
     *valuelen = strlen(kStatic[idx][1]);
   } else {
-    const Entry &e = inf->table[idx - kStaticLen];
-    *name = (const uint8_t *)e.name.data();
-    *namelen = e.name.size();
-    *value = (const uint8_t *)e.value.data();
-    *valuelen = e.value.size();
+    const DynTable::Ent &e = inf->table.newest(idx - kStaticLen);
+    *name = inf->table.name(e);
+    *namelen = e.nl;
+    *value = inf->table.value(e);
+    *valuelen = e.vl;
   }
   return 0;
 }
@@ -586,7 +656,10 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     snap.reserve(conns.size());
     for (auto *c : conns) snap.push_back(*c);
   }
-  std::vector<BlockOut> outs(nblocks);
+  // per-block field buffers, kept across calls (under the engine's lock):
+  // replay allocates only while they grow
+  std::vector<BlockOut> &outs = E.outs;
+  if (outs.size() < nblocks) outs.resize(nblocks);
   parallel_for(conns.size(), 1, [&](size_t c) {
     for (uint32_t i : lists[c]) replay_block(conns[c], bl[i], ls, outs[i]);
   });

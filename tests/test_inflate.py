@@ -273,3 +273,51 @@ def test_inflate_buffer_cut_rolls_back_cpu():
                                          arena_cap=6000)
     for k in range(cut, len(blocks)):
         assert (st2[k - cut], f2[k - cut]) == refs[order[k]].inflate_block(blocks[k]), k
+
+
+# ---- the dynamic table's byte ring (csrc/hd_inflate.cpp DynTable): long
+# runs that wrap it many times, size updates that shrink and regrow it, and
+# an insertion whose name comes from the entry it evicts ----
+def test_inflate_table_ring_wraps_and_resizes_cpu():
+    import nghttp2_amd
+    rng = np.random.Generator(np.random.PCG64(0x5EED1))
+    nconn = 3
+    infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+    refs = [HO.Inflater() for _ in range(nconn)]
+    enc_tables = [[] for _ in range(nconn)]
+    table_max = [4096] * nconn
+    for rnd in range(60):
+        order, blocks = [], []
+        for c in rng.permutation(nconn):
+            pre = b""
+            if rng.random() < 0.25:  # a table size update at the block head
+                table_max[c] = int(rng.choice([0, 50, 300, 1000, 2500, 4096]))
+                pre = bytes(O.encode_length(table_max[c], 5, 0x20))
+                t, size = enc_tables[c], sum(len(a) + len(b) + 32 for a, b in enc_tables[c])
+                while size > table_max[c] and t:
+                    a, b = t.pop()
+                    size -= len(a) + len(b) + 32
+            fields = _random_fields(rng, int(rng.integers(1, 14)))
+            blocks.append(pre + _encode_block(rng, enc_tables[c], fields, table_max[c], huff_p=0.0))
+            order.append(int(c))
+        st, f = nghttp2_amd.inflate_blocks([infs[c] for c in order], blocks)
+        for k, (c, blk) in enumerate(zip(order, blocks)):
+            assert (st[k], f[k]) == refs[c].inflate_block(blk), (rnd, k, c)
+    for c in range(nconn):
+        assert infs[c].dynamic_table() == [tuple(e) for e in refs[c].table], c
+        assert infs[c].dynamic_table_size() == sum(len(a) + len(b) + 32 for a, b in refs[c].table)
+
+
+def test_inflate_name_from_evicted_entry_cpu():
+    """Literal with incremental indexing whose indexed name is the entry its
+    own insertion evicts (lib/nghttp2_hd.c add_hd_table_incremental copies
+    the name first)."""
+    import nghttp2_amd
+    inf, ref = nghttp2_amd.HpackInflater(), HO.Inflater()
+    blk = bytes(O.encode_length(100, 5, 0x20))  # table of 100 bytes
+    blk += b"\x40" + bytes(O.encode_length(4, 7, 0)) + b"aaaa" + bytes(O.encode_length(40, 7, 0)) + b"v" * 40
+    blk += bytes(O.encode_length(62, 6, 0x40)) + bytes(O.encode_length(41, 7, 0)) + b"w" * 41
+    blk += bytes(O.encode_length(62, 6, 0x40)) + bytes(O.encode_length(0, 7, 0))
+    st, f = nghttp2_amd.inflate_blocks([inf], [blk])
+    assert (st[0], f[0]) == ref.inflate_block(blk)
+    assert inf.dynamic_table() == [(b"aaaa", b"")] == [tuple(e) for e in ref.table]

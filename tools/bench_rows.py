@@ -109,9 +109,11 @@ def bench_names(steps=50, long_frac=0.02):
             "Gnames_per_s": round(n / t / 1e9, 3), "long_wave_frac": long_frac}
 
 
-def make_blocks(nconn, per_conn, fields_per_block, seed=7):
+def make_blocks(nconn, per_conn, fields_per_block, seed=7, index=False):
     """Header blocks of two indexed static fields and `fields_per_block`
-    literal fields without indexing, new name (Huffman when shorter)."""
+    literal fields with a new name (Huffman when shorter), without indexing
+    or (`index`) with incremental indexing, so every field enters the
+    connection's dynamic table and evicts older ones."""
     from oracle import oracle as O
     from nghttp2_amd import workloads as W
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -126,7 +128,7 @@ def make_blocks(nconn, per_conn, fields_per_block, seed=7):
                 name = names[rng.integers(0, len(names))]
                 val = bytes(pool[off[v]:off[v + 1]])
                 v += 1
-                out.append(0x00)  # literal without indexing, new name
+                out.append(0x40 if index else 0x00)  # literal, new name
                 out += O.emit_string(name)
                 out += O.emit_string(val)
             blocks.append(bytes(out))
@@ -134,25 +136,28 @@ def make_blocks(nconn, per_conn, fields_per_block, seed=7):
     return blocks, conns
 
 
-def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
+def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5, index=False):
     """The batched inflate front-end on `nconn` connections x `per_conn`
     blocks of `fields` literal fields: the C call alone
     (nghttp2_amd_hd_inflate_blocks: host parse, one GPU decode of every
     Huffman literal with its H2D/D2H, host replay, placement), timed around
     the ctypes call with the arrays built once, and the Python wrapper
     (inflate_blocks: marshalling the blocks in and the fields out) around it.
-    The blocks insert nothing into the tables, so repeated calls see the
-    same state."""
+    Without `index` the blocks insert nothing into the tables, so repeated
+    calls see the same state; with it every call starts from fresh
+    inflaters (made outside the timed region)."""
     import ctypes
     import nghttp2_amd
     from nghttp2_amd import hd
     from oracle import hpack_oracle as HO
-    blocks, conns = make_blocks(nconn, per_conn, fields)
+    blocks, conns = make_blocks(nconn, per_conn, fields, index=index)
     wire = sum(len(b) for b in blocks)
     infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
     # the wrapper, parity on the first connection's blocks against the restatement
     best_py = None
-    for _ in range(reps):
+    for r in range(reps):
+        if index and r:
+            infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
         t0 = time.perf_counter()
         st, f = nghttp2_amd.inflate_blocks([infs[c] for c in conns], blocks)
         t = time.perf_counter() - t0
@@ -178,6 +183,9 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     best_c = None
     for _ in range(3 * reps):
+        if index:
+            fresh = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+            ip = (ctypes.c_void_p * m)(*[fresh[c].p.value for c in conns])
         t0 = time.perf_counter()
         rv = L.nghttp2_amd_hd_inflate_blocks(ip, m, ptrs, lens, nva, nva_cap, ctypes.byref(nv_used),
                                              arena, arena_cap, ctypes.byref(ar_used), stc, s)
@@ -186,6 +194,7 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
         best_c = t if best_c is None or t < best_c else best_c
     assert list(stc) == list(st)
     return {"blocks": len(blocks), "connections": nconn, "fields": nf, "wire_bytes": wire,
+            "incremental_indexing": index,
             "c_s_per_call": round(best_c, 5), "c_wire_MBps": round(wire / best_c / 1e6, 1),
             "c_fields_per_s": round(nf / best_c),
             "py_s_per_call": round(best_py, 4), "py_wire_MBps": round(wire / best_py / 1e6, 1),
@@ -197,6 +206,7 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5):
 if __name__ == "__main__":
     rows = sys.argv[1:] or ["emit", "emit3", "inflate", "names"]
     fns = {"emit": bench_emit, "emit3": lambda: bench_emit(cfg=3), "inflate": bench_inflate,
+           "inflate_index": lambda: bench_inflate(index=True),
            "names": bench_names,
            "names_short": lambda: bench_names(long_frac=0.0)}
     print(json.dumps({r: fns[r]() for r in rows}, indent=1))
