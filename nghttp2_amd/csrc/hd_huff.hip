@@ -318,14 +318,15 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
                                                   uint32_t *__restrict__ tile_sums,
-                                                  int bits_out) {
+                                                  int bits_out, uint32_t tile0) {
+  const uint32_t tb = tile0 + blockIdx.x;  // this workgroup's tile
   __shared__ uint8_t lenT[256];
   __shared__ alignas(16) uint32_t pre[EC_CNT_NT / 64][512];  // a round's prefixes (u16 per byte)
   __shared__ uint32_t red[2 * EC_CNT_NT / 64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   if (threadIdx.x < 256) lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
   __syncthreads();
-  const uint32_t t0 = blockIdx.x * WG + EC_CNT_SPW * wv;  // the wave's strings
+  const uint32_t t0 = tb * WG + EC_CNT_SPW * wv;  // the wave's strings
   uint32_t e = 0;
   bool huge = false;
   if (t0 < n) {
@@ -355,18 +356,10 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
       q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
       if (cb + 64u * EC_CNT_PFD + lane < c_end)
         q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
-#if defined(DE_ABL_CNT_STREAM)  // diag: the loads alone (wrong counts; timing only)
-      Rc += wd[0] ^ wd[1] ^ wd[2] ^ wd[3];
-      continue;
-#endif
       uint32_t run = 0, pk[8];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-#if defined(DE_ABL_CNT_NOLUT)  // diag: no length lookups (wrong counts; timing only)
-        const uint32_t L = (wd[j >> 2] >> (8 * (j & 3))) & 0x7u;
-#else
         const uint32_t L = lenT[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-#endif
         if (j & 1) pk[j >> 1] |= run << 16; else pk[j >> 1] = run;
         run += L;
       }
@@ -415,7 +408,7 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
     // and every one after it overflow in k_encode.  (Round 4: 64-bit bit
     // positions in k_encode instead cost 8.7 us of 140 on config 3.)
     block_excl_scan_sum<EC_CNT_NT>(e, huge ? 0x2000u : e >> 16, red, &tot, &hi);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = hi >= 0x2000u - WG ? 0xFFFFFFFFu : tot;
+    if (threadIdx.x == 0) tile_sums[tb] = hi >= 0x2000u - WG ? 0xFFFFFFFFu : tot;
   }
 }
 
@@ -433,6 +426,9 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
+#ifndef EC_WIN
+#define EC_WIN 0x7FFFFFFFu  // tiles per count+pack window (diag A/B; default: one window)
+#endif
 #ifndef EC_WPE
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
 #endif
@@ -466,7 +462,9 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_sums) {
+                                               const uint32_t *__restrict__ tile_sums,
+                                               uint32_t tile0) {
+  const uint32_t tb = tile0 + blockIdx.x;  // this workgroup's tile
   constexpr uint32_t RW = FR ? EC_RW_F : EC_RW;
   constexpr uint32_t PDW = FR ? 512u : 256u;  // u16 extras / u8 pads per round byte
   __shared__ uint2 codeT[256];  // {code MSB-aligned, length}
@@ -485,9 +483,9 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   lds_u32 *rwm = (lds_u32 *)rawm[wv];
 #pragma unroll
   for (uint32_t i = 0; i < PDW / 64u; ++i) pdw[lane + 64u * i] = 0u;
-  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
+  const uint32_t s_me = tb * WG + threadIdx.x;
   const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
-  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
+  const uint32_t t0 = tb * WG + 64u * wv;
   const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
   const bool sl = lane < nstr;
   const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
@@ -510,11 +508,11 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   {
     uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t t = threadIdx.x;
-    for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
+    for (; t + 7u * WG < tb; t += 8u * WG) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) p8[k] += tile_sums[t + k * WG];
     }
-    for (; t < blockIdx.x; t += WG) pre += tile_sums[t];
+    for (; t < tb; t += WG) pre += tile_sums[t];
 #pragma unroll
     for (int k = 0; k < 8; ++k) pre += p8[k];
   }
@@ -524,7 +522,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                &ptot_lo);  // (barriers)
   // (a string too long for the 32-bit code-bit counts poisoned the tile's
   // sum: the tile overflows)
-  const uint64_t tot = tile_sums[blockIdx.x] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
+  const uint64_t tot = tile_sums[tb] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
   {
     uint32_t dummy;
     block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
@@ -623,11 +621,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
         uint32_t c[4], l[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-#ifndef DE_ABL_NOLUT
           const uint2 cj = *(const uint2 *)((const char *)codeT + EC_B8(4 * m + u));
-#else
-          const uint2 cj = make_uint2(EC_B8(4 * m + u) << 21, 5u + ((EC_B8(4 * m + u) >> 3) & 1u));
-#endif
           c[u] = cj.x;
           l[u] = cj.y + ((pd[m] >> (8 * u)) & 0xFFu);
         }
@@ -686,11 +680,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
         uint32_t b = ib0;
 #pragma unroll
         for (int m = 0; m < (FR ? 8 : 4); ++m) {
-#ifndef DE_ABL_NOOR
           ec_or3(img, b, qh[m], qo[m]);
-#else
-          if (qh[m] == 0x12345u) img[b >> 5] = qo[m];  // (keep the quads live)
-#endif
           b += ql[m];
         }
       } else {  // a code of <= 37 bits, MSB-aligned in 64; one dword at a time
@@ -1341,11 +1331,6 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
                    // round 3 with overshooting warm-ups, 16/18/22: 312.4/308.9/304.8 vs 300.8)
 #define DD_TASK_W 32u  // a string's weight in bytes when balancing tasks over workgroups
 #define DD_NONE 0xFFFFFFFCu  // a round's carried exit: the last item ended its string
-#if defined(DD_ABL_NOOUT) || defined(DD_ABL_NOSTORE)
-#define DD_NOOUT_ON true
-#else
-#define DD_NOOUT_ON false
-#endif
 #ifndef DD_IW64
 #define DD_IW64 16
 #endif
@@ -1386,11 +1371,7 @@ template <uint32_t IP, int IW, int LB, uint32_t BI = 0>
 struct DIShared {  // k_decode_items
   DecT<LB> T;  // first: the lookup at LDS offset 0
   alignas(16) uint32_t ib[IW][di_ibw(di_span(IP, BI))];
-#ifdef DD_ABL_NOOUT
-  alignas(16) uint32_t ob[IW][4];
-#else
   alignas(16) uint32_t ob[IW][(di_obb(IP, BI) / 4 + 1 + 3) & ~3u];
-#endif
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
   uint32_t claimed;               // tasks of the workgroup's range claimed so far
@@ -1414,12 +1395,8 @@ struct LdsPtrSink {
     // (round 3: one ds_write_b16 at the byte address -- the LDS runs in
     // unaligned mode, tools/diag/probe -- measured slower: 354.9 vs 296.2 us
     // on config 3, the hardware splits misaligned stores)
-#ifndef DD_ABL_NOOUT
     p[0] = (uint8_t)v;
     p[1] = (uint8_t)(v >> 16);
-#else
-    (void)v;
-#endif
     p += c8 >> 3;
   }
   __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
@@ -1429,42 +1406,7 @@ struct LdsPtrSink {
   __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
   __device__ __forceinline__ void flush() {}
 };
-// Output gathered in a register word and written one dword per step (pair):
-// w = the step's 1-4 bytes, appended to the pending bytes `acc` (nb bits);
-// the dword at q is (re)written each step with what it holds so far and q
-// advances when it is full.  One ds_write_b32 instead of two ds_write_b8 per
-// entry: ~10 more VALU per pair, 12 LDS-store cycles less.
-struct AccSink {
-  lds_u32 *q, *base;
-  uint32_t acc, nb;
-  __device__ __forceinline__ AccSink(lds_u8 *b) : q((lds_u32 *)b), base((lds_u32 *)b), acc(0), nb(0) {}
-  __device__ __forceinline__ uint32_t count() const { return 4u * (uint32_t)(q - base) + (nb >> 3); }
-  __device__ __forceinline__ void add(uint32_t w, uint32_t cw) {
-    const uint32_t lo = acc | (w << nb);
-    const uint32_t hi = __builtin_amdgcn_alignbit(w, 0u, 32u - nb);  // (nb = 0: 0)
-    *q = lo;
-    const uint32_t t = nb + cw;
-    const bool full = t >= 32u;
-    q += full ? 1 : 0;
-    acc = full ? hi : lo;
-    nb = t & 31u;
-  }
-  __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
-    add(__builtin_amdgcn_perm(0u, v, 0x0C0C0200u), c8);
-  }
-  __device__ __forceinline__ void put2(uint32_t e1, uint32_t e2) {
-    const uint32_t c1 = E_CNT8(e1);
-    add(__builtin_amdgcn_perm(0u, e1, 0x0C0C0200u) | (__builtin_amdgcn_perm(0u, e2, 0x0C0C0200u) << c1),
-        c1 + E_CNT8(e2));
-  }
-  __device__ __forceinline__ void put(uint32_t v, uint32_t c8) { put_nf(v, c8); }
-  __device__ __forceinline__ void flush() {}
-};
-#ifdef DD_ACC2
-typedef AccSink DISink;
-#else
 typedef LdsPtrSink DISink;
-#endif
 
 // the item decoder's 16-byte input loads and output stores
 __device__ __forceinline__ uint4 dd_ld16(const uint4 *p) { return *p; }
@@ -1704,29 +1646,6 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
   }
 }
 
-#ifdef DD_STAMPS
-// Diagnostic build only (tools/diag/stamps.py): per-phase shader-clock
-// sums of the item decoder's waves, read back by nghttp2_amd_hd__stamps.
-__device__ unsigned long long dd_stamps[16];
-#define DD_STAMP_INIT() uint64_t st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_prev_ = __builtin_amdgcn_s_memtime()
-#define DD_STAMP(k)                                        \
-  do {                                                     \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
-    st_acc_[k] += t_ - st_prev_;                           \
-    st_prev_ = t_;                                         \
-  } while (0)
-#define DD_STAMP_COUNT(k) (st_acc_[k] += 1)
-#define DD_STAMP_FLUSH()                                                   \
-  do {                                                                     \
-    if (lane == 0)                                                         \
-      for (int k_ = 0; k_ < 10; ++k_) atomicAdd(&dd_stamps[k_], (unsigned long long)st_acc_[k_]); \
-  } while (0)
-#else
-#define DD_STAMP_INIT() do {} while (0)
-#define DD_STAMP(k) do {} while (0)
-#define DD_STAMP_COUNT(k) do {} while (0)
-#define DD_STAMP_FLUSH() do {} while (0)
-#endif
 
 // ---------------------------------------------------------------------------
 // Dense decode by items (decode_batch_auto): a string of <= DD_P encoded
@@ -1761,7 +1680,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   if (threadIdx.x == 0) S.claimed = 0u;
   stage_dec_tables(S.T, (WAVE * IW));  // the kernel's only workgroup barrier
   const uint32_t off0 = off[0];
-  DD_STAMP_INIT();
   const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
   // this workgroup's tasks: with 40-byte pieces (long values, whose tasks
   // differ several-fold in work) a contiguous range balanced by weight
@@ -1855,9 +1773,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
     lds_u32 *smap = (lds_u32 *)S.smap[wv];
     uint32_t R0 = A;
-    DD_STAMP(0);  // task setup
     for (uint32_t r0 = 0, nv = 0; r0 < M; r0 += nv) {
-      DD_STAMP_COUNT(8);
       nv = min(M - r0, (uint32_t)WAVE);  // (budgeted rounds: cut below)
       const uint32_t q = r0 + lane;
       // this lane's item: its string i = the last one with X_i <= q; every
@@ -1898,7 +1814,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const bool valid = lane < nv;
       const bool last = e == b;
       const bool spec = valid && k > 0;
-      DD_STAMP(1);  // item map
       // ---- stage [first item (- OV), last item's end + 8)
       uint32_t IB, nchunk;
       round_range(R0, A, Z, IB, nchunk);
@@ -1930,7 +1845,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             if (lane + WAVE * u < nchunk) pf[u] = dd_ld16(g + lane + WAVE * u);
         }
         stage_pf(nchunk);
-        DD_STAMP(9);  // staging: the wait for the prefetched chunks and their LDS writes
         // prefetch the next round: of this task, else the next task's first
         pf_IB = 0xFFFFFFFFu;
         uint32_t IBn = 0, ncn = 0;
@@ -1957,7 +1871,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
       const uint32_t bstop = last ? bend : 8u * (e - IBX);
       DISink sk(my_ob);
-      DD_STAMP(2);  // staging
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
@@ -1968,7 +1881,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         entry = bp;
         dead = rw.failed;
       }
-      DD_STAMP(3);  // warm-up
       // ---- the item's symbols
       uint32_t bp = entry;
       DDRun rr;
@@ -2023,7 +1935,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           my_entry = pred;
         }
       }
-      DD_STAMP(4);  // decode + verify
       // ---- string symbol counts: segmented scan (heads: first items)
       // (the plain inclusive scan of the lanes' byte counts, less its value
       // before the lane's last head; no head yet: plus the carried count)
@@ -2039,7 +1950,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // ---- dense placement
       const uint32_t O_l = run + Tinc - V;
       if (valid && k == 0) ost[i] = O_l;
-      DD_STAMP(5);  // scans + finish
       // ---- store: each lane stores its region straight to its output bytes
       // with unaligned stores (gfx950 global memory takes them whole):
       // 16-byte pieces, then the tail as 8-, 4-, 2- and 1-byte pieces.
@@ -2047,35 +1957,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // alignbyte with bytewise heads and tails, or for 64-byte items
       // compacted in LDS and stored 16 bytes per lane: config 3 decode
       // 249.6 -> 238.9 us, config 2 48.0 -> 43.3, config 5 130.4 -> 124.5.)
-#if defined(DD_ABL_NOOUT) || defined(DD_ABL_NOSTORE)
-      if (false) {
-#else
       {
-#endif
         const uint64_t g0 = tbase + O_l;
         const bool fits = g0 + V <= dst_cap;
         const uint32_t n16 = fits ? V >> 4 : 0u;
         const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(n16), 63);
-#if defined(DD_ABL_COALST)
-        {  // ablation: the round's bytes stored contiguously, 16 B per lane (garbage order)
-          const uint32_t Tot = __builtin_amdgcn_readlane(Tinc, 63);
-          const uint64_t G = (tbase + run) & ~15ull;
-          for (uint32_t c = lane; 16u * c < Tot + 16u; c += WAVE) {
-            u32x4 v;
-            v.x = my_ob32[(4u * c) & 15u];
-            v.y = my_ob32[(4u * c + 1u) & 15u];
-            v.z = my_ob32[(4u * c + 2u) & 15u];
-            v.w = my_ob32[(4u * c + 3u) & 15u];
-            if (G + 16u * c + 16u <= dst_cap) *(u32x4 *)(dst + G + 16u * c) = v;
-          }
-        }
-        if (false) {
-#endif
-#ifdef DD_ABL_ALIGNST
-        uint8_t *o = dst + (g0 & ~15ull);
-#else
         uint8_t *o = dst + g0;
-#endif
 #pragma unroll
         for (uint32_t m = 0; m < (di_rb(IP) + 15u) / 16u; ++m) {
           if (m >= mx) break;
@@ -2108,11 +1995,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           for (uint32_t x = 0; x < V; ++x)
             if (g0 + x < dst_cap) dst[g0 + x] = my_ob[x];
         }
-#if defined(DD_ABL_COALST)
-        }
-#endif
       }
-      DD_STAMP(6);  // store
       run += __builtin_amdgcn_readlane(Tinc, 63);
       R0 = __builtin_amdgcn_readlane(e, nv - 1u);
       carry_exit = __builtin_amdgcn_readlane(last ? DD_NONE : my_exit, nv - 1u);
@@ -2129,10 +2012,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    DD_STAMP(7);  // round tails + epilogue
     task = next_task;
   }
-  DD_STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -2333,7 +2214,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_enc_count<false>, dim3(ntiles_for(n)), dim3(EC_CNT_NT), 0, (hipStream_t)stream, src,
-                     src_off, n, enc_len, (uint32_t *)nullptr, 0);
+                     src_off, n, enc_len, (uint32_t *)nullptr, 0, 0u);
   return hip_rv(hipGetLastError());
 }
 
@@ -2349,9 +2230,12 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
-  hipLaunchKernelGGL(k_encode<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+  for (uint32_t w0 = 0; w0 < nt; w0 += EC_WIN) {
+    const uint32_t wn = min(nt - w0, (uint32_t)EC_WIN);
+    hipLaunchKernelGGL(k_enc_count<false>, dim3(wn), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1, w0);
+    hipLaunchKernelGGL(k_encode<false>, dim3(wn), dim3(WG), 0, st, src, src_off, n, dst,
+                       (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, w0);
+  }
   return hip_rv(hipGetLastError());
 }
 
@@ -2384,9 +2268,12 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
-  hipLaunchKernelGGL(k_encode<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+  for (uint32_t w0 = 0; w0 < nt; w0 += EC_WIN) {
+    const uint32_t wn = min(nt - w0, (uint32_t)EC_WIN);
+    hipLaunchKernelGGL(k_enc_count<true>, dim3(wn), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1, w0);
+    hipLaunchKernelGGL(k_encode<true>, dim3(wn), dim3(WG), 0, st, src, src_off, n, dst,
+                       (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, w0);
+  }
   return hip_rv(hipGetLastError());
 }
 
@@ -2430,17 +2317,6 @@ int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off
   return hip_rv(hipGetLastError());
 }
 
-#ifdef DD_STAMPS
-NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__stamps(uint64_t *out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dd_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
-    return NGHTTP2_AMD_ERR_FATAL;
-  if (reset) {
-    unsigned long long z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(dd_stamps), z, sizeof z) != hipSuccess) return NGHTTP2_AMD_ERR_FATAL;
-  }
-  return 0;
-}
-#endif
 
 int nghttp2_amd_hd_huff_decode_batch_auto(const uint8_t *src, const uint32_t *src_off,
                                           uint32_t n, uint64_t enc_bytes, uint8_t *dst,

@@ -4,16 +4,28 @@
 # Usage: build_variants.sh name:"-DFLAG=1 -DX=2" ...   (name "cur" = no flags)
 # hd_huff.hip builds as its two translation units (the decoders with
 # DEC_SCHED), as the Makefile does.  REV=<git rev> builds every variant from
-# that revision's sources instead of the working tree.
+# that revision's sources instead of the working tree.  PATCH="<file> ..."
+# applies patches to a copy of the sources first: the ablation and stamp
+# hooks (DD_ABL_*, DE_ABL_*, DD_ACC2, DD_STAMPS) live in
+# patches/r4_diag_hooks.patch, not in the product source.
 set -e
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$HERE/../..
+T=""
 if [ -n "${REV:-}" ]; then
   T=$(mktemp -d)
   (cd $ROOT && git archive $REV nghttp2_amd/csrc include | tar -x -C $T)
   C=$T/nghttp2_amd/csrc
 else
   C=$ROOT/nghttp2_amd/csrc
+fi
+if [ -n "${PATCH:-}" ]; then
+  if [ -z "$T" ]; then
+    T=$(mktemp -d)
+    mkdir -p $T/nghttp2_amd && cp -r $ROOT/nghttp2_amd/csrc $T/nghttp2_amd/ && cp -r $ROOT/include $T/
+    C=$T/nghttp2_amd/csrc
+  fi
+  for p in $PATCH; do patch -s -p1 -d $T < $(cd $ROOT && realpath $p); done
 fi
 F="-O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=gfx950"
 DEC_SCHED=${DEC_SCHED:--mllvm -amdgpu-sched-strategy=max-ilp}
@@ -31,5 +43,5 @@ for spec in "$@"; do
   ) &
 done
 wait
-[ -n "${REV:-}" ] && rm -rf $T
+[ -n "$T" ] && rm -rf $T
 ls $HERE/lib_*.so

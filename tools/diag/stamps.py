@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Per-phase shader-clock breakdown of the item decoder (a DD_STAMPS build of
-the engine, tools/diag/lib_stamps.so from build_variants.sh): task setup, item map, staging,
+the engine, tools/diag/lib_stamps.so from
+`PATCH=tools/diag/patches/r4_diag_hooks.patch build_variants.sh stamps:-DDD_STAMPS`):
+task setup, item map, staging,
 warm-up, decode + verify, scans + finish, store, round tails.  Cycles per
 wave-round and shares, per config.  The stamps themselves cost ~10 %."""
 import ctypes, json, os, sys
