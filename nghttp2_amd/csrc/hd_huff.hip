@@ -318,15 +318,14 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
                                                   uint32_t n,
                                                   uint32_t *__restrict__ out_len,
                                                   uint32_t *__restrict__ tile_sums,
-                                                  int bits_out, uint32_t tile0) {
-  const uint32_t tb = tile0 + blockIdx.x;  // this workgroup's tile
+                                                  int bits_out) {
   __shared__ uint8_t lenT[256];
   __shared__ alignas(16) uint32_t pre[EC_CNT_NT / 64][512];  // a round's prefixes (u16 per byte)
   __shared__ uint32_t red[2 * EC_CNT_NT / 64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   if (threadIdx.x < 256) lenT[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
   __syncthreads();
-  const uint32_t t0 = tb * WG + EC_CNT_SPW * wv;  // the wave's strings
+  const uint32_t t0 = blockIdx.x * WG + EC_CNT_SPW * wv;  // the wave's strings
   uint32_t e = 0;
   bool huge = false;
   if (t0 < n) {
@@ -408,7 +407,7 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
     // and every one after it overflow in k_encode.  (Round 4: 64-bit bit
     // positions in k_encode instead cost 8.7 us of 140 on config 3.)
     block_excl_scan_sum<EC_CNT_NT>(e, huge ? 0x2000u : e >> 16, red, &tot, &hi);
-    if (threadIdx.x == 0) tile_sums[tb] = hi >= 0x2000u - WG ? 0xFFFFFFFFu : tot;
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = hi >= 0x2000u - WG ? 0xFFFFFFFFu : tot;
   }
 }
 
@@ -426,9 +425,6 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
-#ifndef EC_WIN
-#define EC_WIN 0x7FFFFFFFu  // tiles per count+pack window (diag A/B; default: one window)
-#endif
 #ifndef EC_WPE
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
 #endif
@@ -462,9 +458,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_sums,
-                                               uint32_t tile0) {
-  const uint32_t tb = tile0 + blockIdx.x;  // this workgroup's tile
+                                               const uint32_t *__restrict__ tile_sums) {
   constexpr uint32_t RW = FR ? EC_RW_F : EC_RW;
   constexpr uint32_t PDW = FR ? 512u : 256u;  // u16 extras / u8 pads per round byte
   __shared__ uint2 codeT[256];  // {code MSB-aligned, length}
@@ -483,9 +477,9 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   lds_u32 *rwm = (lds_u32 *)rawm[wv];
 #pragma unroll
   for (uint32_t i = 0; i < PDW / 64u; ++i) pdw[lane + 64u * i] = 0u;
-  const uint32_t s_me = tb * WG + threadIdx.x;
+  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
   const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
-  const uint32_t t0 = tb * WG + 64u * wv;
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
   const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
   const bool sl = lane < nstr;
   const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
@@ -508,11 +502,11 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   {
     uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t t = threadIdx.x;
-    for (; t + 7u * WG < tb; t += 8u * WG) {
+    for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) p8[k] += tile_sums[t + k * WG];
     }
-    for (; t < tb; t += WG) pre += tile_sums[t];
+    for (; t < blockIdx.x; t += WG) pre += tile_sums[t];
 #pragma unroll
     for (int k = 0; k < 8; ++k) pre += p8[k];
   }
@@ -522,7 +516,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                &ptot_lo);  // (barriers)
   // (a string too long for the 32-bit code-bit counts poisoned the tile's
   // sum: the tile overflows)
-  const uint64_t tot = tile_sums[tb] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
+  const uint64_t tot = tile_sums[blockIdx.x] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
   {
     uint32_t dummy;
     block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
@@ -2214,7 +2208,7 @@ int nghttp2_amd_hd_huff_encode_count_batch(const uint8_t *src, const uint32_t *s
   if (n == 0) return 0;
   if (!src || !src_off || !enc_len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   hipLaunchKernelGGL(k_enc_count<false>, dim3(ntiles_for(n)), dim3(EC_CNT_NT), 0, (hipStream_t)stream, src,
-                     src_off, n, enc_len, (uint32_t *)nullptr, 0, 0u);
+                     src_off, n, enc_len, (uint32_t *)nullptr, 0);
   return hip_rv(hipGetLastError());
 }
 
@@ -2230,12 +2224,9 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  for (uint32_t w0 = 0; w0 < nt; w0 += EC_WIN) {
-    const uint32_t wn = min(nt - w0, (uint32_t)EC_WIN);
-    hipLaunchKernelGGL(k_enc_count<false>, dim3(wn), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1, w0);
-    hipLaunchKernelGGL(k_encode<false>, dim3(wn), dim3(WG), 0, st, src, src_off, n, dst,
-                       (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, w0);
-  }
+  hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_encode<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
 }
 
@@ -2268,12 +2259,9 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
-  for (uint32_t w0 = 0; w0 < nt; w0 += EC_WIN) {
-    const uint32_t wn = min(nt - w0, (uint32_t)EC_WIN);
-    hipLaunchKernelGGL(k_enc_count<true>, dim3(wn), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1, w0);
-    hipLaunchKernelGGL(k_encode<true>, dim3(wn), dim3(WG), 0, st, src, src_off, n, dst,
-                       (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, w0);
-  }
+  hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
+  hipLaunchKernelGGL(k_encode<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
   return hip_rv(hipGetLastError());
 }
 
