@@ -22,6 +22,8 @@ import collections
 import ctypes
 import os
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnghttp2_amd_hd.so"
 
@@ -407,18 +409,31 @@ class HpackInflater:
         return self.L.nghttp2_amd_hd_inflate_get_dynamic_table_size(self.p)
 
 
+_NV_DTYPE = np.dtype([("block", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
+                      ("value_off", "<u4"), ("value_len", "<u4"), ("flags", "u1")], align=True)
+assert _NV_DTYPE.itemsize == ctypes.sizeof(_Nv)
+
+
 def inflate_blocks(inflaters, blocks, stream=None, nva_cap=None, arena_cap=None, retry=True):
     """Inflate complete header blocks, block i against inflaters[i], with
     every Huffman literal decoded in one GPU batch.  Returns
     (status[i], fields[i] = [(name, value, flags)]).  A batch that outgrows
     the field/arena buffers is cut at the first block that does not fit
     (status NGHTTP2_ERR_BUFFER_ERROR from there on, those blocks not
-    applied); with retry the rest is resubmitted with buffers twice the size."""
+    applied); with retry the rest is resubmitted with buffers twice the size.
+    The blocks go in as one joined buffer and the fields come out of
+    uninitialised numpy buffers (no per-block ctypes objects, no zero fill)."""
     L = _inflate_lib()
     nb = len(blocks)
-    bufs = [bytes(b) for b in blocks]
-    keep = [ctypes.create_string_buffer(b, max(1, len(b))) for b in bufs]
-    total = sum(len(b) for b in bufs)
+    joined = b"".join(bytes(b) for b in blocks)
+    total = len(joined)
+    lens_all = np.fromiter((len(b) for b in blocks), dtype=np.uint64, count=nb)
+    starts = np.zeros(nb, dtype=np.uint64)
+    if nb > 1:
+        np.cumsum(lens_all[:-1], out=starts[1:])
+    pool = np.frombuffer(joined, dtype=np.uint8) if total else np.zeros(1, dtype=np.uint8)
+    ptrs_all = starts + np.uint64(pool.ctypes.data)
+    infs_all = np.fromiter((i.p.value for i in inflaters), dtype=np.uint64, count=nb)
     nva_cap = total + 16 if nva_cap is None else nva_cap
     arena_cap = 8 * total + 64 * (total + 16) + 4096 if arena_cap is None else arena_cap
     s = None
@@ -434,28 +449,32 @@ def inflate_blocks(inflaters, blocks, stream=None, nva_cap=None, arena_cap=None,
     status = [NGHTTP2_ERR_BUFFER_ERROR] * nb
     fields = [[] for _ in range(nb)]
     first = 0
+    vp = ctypes.c_void_p
     while first < nb:
         m = nb - first
-        ptrs = (ctypes.c_void_p * m)(*[ctypes.cast(k, ctypes.c_void_p) for k in keep[first:]])
-        lens = (ctypes.c_size_t * m)(*[len(b) for b in bufs[first:]])
-        infs = (ctypes.c_void_p * m)(*[i.p.value for i in inflaters[first:]])
-        nva = (_Nv * max(1, nva_cap))()
-        arena = (ctypes.c_uint8 * max(1, arena_cap))()
-        st = (ctypes.c_int32 * m)()
+        ptrs = np.ascontiguousarray(ptrs_all[first:])
+        lens = np.ascontiguousarray(lens_all[first:])
+        infs = np.ascontiguousarray(infs_all[first:])
+        nva = np.empty(max(1, nva_cap), dtype=_NV_DTYPE)
+        arena = np.empty(max(1, arena_cap), dtype=np.uint8)
+        st = np.empty(m, dtype=np.int32)
         nv_used, ar_used = ctypes.c_size_t(), ctypes.c_size_t()
-        rv = L.nghttp2_amd_hd_inflate_blocks(infs, m, ptrs, lens, nva, nva_cap,
-                                             ctypes.byref(nv_used), arena, arena_cap,
-                                             ctypes.byref(ar_used), st, s)
+        rv = L.nghttp2_amd_hd_inflate_blocks(vp(infs.ctypes.data), m, vp(ptrs.ctypes.data),
+                                             vp(lens.ctypes.data), vp(nva.ctypes.data), nva_cap,
+                                             ctypes.byref(nv_used), vp(arena.ctypes.data), arena_cap,
+                                             ctypes.byref(ar_used), vp(st.ctypes.data), s)
         if rv != NGHTTP2_ERR_BUFFER_ERROR:
             _check(rv, "inflate_blocks")
-        raw = bytes(arena[:ar_used.value])
-        for k in range(nv_used.value):
-            r = nva[k]
-            fields[first + r.block].append((raw[r.name_off:r.name_off + r.name_len],
-                                            raw[r.value_off:r.value_off + r.value_len], r.flags))
+        raw = arena[:ar_used.value].tobytes()
+        nv = nva[:nv_used.value]
+        for b, no, nl, vo, vl, fl in zip((nv["block"] + first).tolist(), nv["name_off"].tolist(),
+                                         nv["name_len"].tolist(), nv["value_off"].tolist(),
+                                         nv["value_len"].tolist(), nv["flags"].tolist()):
+            fields[b].append((raw[no:no + nl], raw[vo:vo + vl], fl))
+        stl = st.tolist()
         done = 0
-        while done < m and st[done] != NGHTTP2_ERR_BUFFER_ERROR:
-            status[first + done] = st[done]
+        while done < m and stl[done] != NGHTTP2_ERR_BUFFER_ERROR:
+            status[first + done] = stl[done]
             done += 1
         first += done
         if done < m:
@@ -473,6 +492,11 @@ class _NvIn(ctypes.Structure):
     _fields_ = [("name", ctypes.c_void_p), ("value", ctypes.c_void_p),
                 ("namelen", ctypes.c_size_t), ("valuelen", ctypes.c_size_t),
                 ("flags", ctypes.c_uint8)]
+
+
+_NVIN_DTYPE = np.dtype([("name", "<u8"), ("value", "<u8"), ("namelen", "<u8"),
+                        ("valuelen", "<u8"), ("flags", "u1")], align=True)
+assert _NVIN_DTYPE.itemsize == ctypes.sizeof(_NvIn)
 
 
 def _deflate_lib():
@@ -538,24 +562,34 @@ def deflate_blocks(deflaters, header_lists, stream=None):
     nb = len(header_lists)
     flat = [(bytes(h[0]), bytes(h[1]), (h[2] if len(h) > 2 else 0))
             for hl in header_lists for h in hl]
-    keep = []
-    nva = (_NvIn * max(1, len(flat)))()
-    for k, (n_, v_, fl) in enumerate(flat):
-        bn = ctypes.create_string_buffer(n_, max(1, len(n_)))
-        bv = ctypes.create_string_buffer(v_, max(1, len(v_)))
-        keep += [bn, bv]
-        nva[k].name = ctypes.cast(bn, ctypes.c_void_p)
-        nva[k].value = ctypes.cast(bv, ctypes.c_void_p)
-        nva[k].namelen, nva[k].valuelen, nva[k].flags = len(n_), len(v_), fl
-    offs = [0]
-    for hl in header_lists:
-        offs.append(offs[-1] + len(hl))
-    block_off = (ctypes.c_uint32 * (nb + 1))(*offs)
-    cap = sum(len(n_) + len(v_) + 16 for n_, v_, _ in flat) + 16 * nb + 64
-    out = (ctypes.c_uint8 * cap)()
-    out_off = (ctypes.c_uint32 * (nb + 1))()
-    st = (ctypes.c_int32 * max(1, nb))()
-    defl = (ctypes.c_void_p * max(1, nb))(*[d.p.value for d in deflaters])
+    nf = len(flat)
+    # every name and value in one joined buffer; the nv array (nghttp2_nv
+    # layout) points into it -- no ctypes object per field
+    parts = [x for n_, v_, _ in flat for x in (n_, v_)]
+    joined = b"".join(parts)
+    plen = np.fromiter((len(x) for x in parts), dtype=np.uint64, count=2 * nf)
+    pstart = np.zeros(2 * nf, dtype=np.uint64)
+    if nf:
+        np.cumsum(plen[:-1], out=pstart[1:])
+    pool = np.frombuffer(joined, dtype=np.uint8) if joined else np.zeros(1, dtype=np.uint8)
+    nva = np.zeros(max(1, nf), dtype=_NVIN_DTYPE)
+    if nf:
+        base = np.uint64(pool.ctypes.data)
+        nva["name"][:nf] = pstart[0::2] + base
+        nva["value"][:nf] = pstart[1::2] + base
+        nva["namelen"][:nf] = plen[0::2]
+        nva["valuelen"][:nf] = plen[1::2]
+        nva["flags"][:nf] = np.fromiter((f for _, _, f in flat), dtype=np.uint8, count=nf)
+    offs = np.zeros(nb + 1, dtype=np.uint32)
+    if nb:
+        np.cumsum(np.fromiter((len(hl) for hl in header_lists), dtype=np.uint32, count=nb),
+                  out=offs[1:])
+    cap = int(plen.sum()) + 16 * nf + 16 * nb + 64
+    out = np.empty(cap, dtype=np.uint8)
+    out_off = np.zeros(nb + 1, dtype=np.uint32)
+    st = np.zeros(max(1, nb), dtype=np.int32)
+    defl = np.fromiter((d.p.value for d in deflaters), dtype=np.uint64, count=nb) if nb \
+        else np.zeros(1, dtype=np.uint64)
     s = None
     if stream is not None:
         s = ctypes.c_void_p(stream.cuda_stream)
@@ -563,8 +597,12 @@ def deflate_blocks(deflaters, header_lists, stream=None):
         import torch
         if torch.cuda.is_available():
             s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    rv = L.nghttp2_amd_hd_deflate_blocks(defl, nb, nva, block_off, out, cap, out_off, st, s)
+    vp = ctypes.c_void_p
+    rv = L.nghttp2_amd_hd_deflate_blocks(vp(defl.ctypes.data), nb, vp(nva.ctypes.data),
+                                         vp(offs.ctypes.data), vp(out.ctypes.data), cap,
+                                         vp(out_off.ctypes.data), vp(st.ctypes.data), s)
     if rv not in (0, NGHTTP2_ERR_BUFFER_ERROR):
         _check(rv, "deflate_blocks")
-    raw = bytes(out[:out_off[nb]])
-    return [st[i] for i in range(nb)], [raw[out_off[i]:out_off[i + 1]] for i in range(nb)]
+    oo = out_off.tolist()
+    raw = out[:oo[nb]].tobytes()
+    return st[:nb].tolist(), [raw[oo[i]:oo[i + 1]] for i in range(nb)]
