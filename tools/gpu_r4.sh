@@ -5,7 +5,7 @@
 # step has its own limit; a failing step ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r4; mkdir -p $O; export TMPDIR=/tmp
+O=${OUT_DIR:-gpurun_out/r4}; mkdir -p $O; export TMPDIR=/tmp
 run() {
   local name=$1; shift; local t=$1; shift
   echo "== $name (limit ${t}s)"
@@ -33,7 +33,7 @@ for s in ${STEPS:-pytest smoke bench bench5 host prof pmc issue rows}; do
               run pmc_c${c}_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_c$c/p2 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 5 --warmup 2 --config $c
             done ;;
     rows)   rm -rf $O/prof_rows
-            run rows 300 python tools/bench_rows.py emit emit3 inflate names
+            run rows 300 python tools/bench_rows.py emit emit3 inflate inflate_index names
             run prof_rows 300 rocprofv3 --kernel-trace --stats -d $O/prof_rows -o run --output-format csv -- python3 tools/bench_rows.py emit emit3 names ;;
   esac
 done
