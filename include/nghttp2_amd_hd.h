@@ -211,13 +211,18 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, cons
 
 /*
  * Same as nghttp2_amd_hd_huff_decode_batch, with the engine placing the
- * output in the same launch, densely: the strings of each task of 64
- * consecutive strings (t0 = 64 k) are back to back from the task's base
+ * output in the same launch, densely: the batch is cut into tasks of 64
+ * consecutive strings (t0 = 64 k), a task possibly split into two tasks of
+ * 32 (t0 = 64 k, 64 k + 32: the engine splits the last tasks of each
+ * workgroup's share so that its waves finish together), and the strings of
+ * each task are back to back from the task's base
  *   base(t0) = 4 * (ceil(floor(8 x_t0 / 5) / 4) + t0),  x_t0 = src_off[t0] - src_off[0],
  * so dst_off[i] (OUT, n+1 entries) = base(t0) + the decoded bytes of the
- * task's strings before i, and dst_off[n] = the end of the last string.
+ * task's strings before i, and dst_off[n] = the end of the last string
+ * (dst_off is authoritative; which tasks were split is not specified).
  * Every string keeps the reference's allocation inside its task's span
- * (base(t0 + 64) - base(t0) >= the sum of floor(8 E_i / 5) + 1), so no
+ * (base(t1) - base(t0) >= the sum of floor(8 E_i / 5) + 1 over the task
+ * [t0, t1)), so no
  * string can overflow; bytes between the end of a task's output and the
  * next task's base are unspecified.  dst (16-byte aligned) must hold
  * nghttp2_amd_hd_huff_decode_bound(E_total, n) bytes.  String i gets -502

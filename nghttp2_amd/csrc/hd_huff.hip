@@ -817,10 +817,13 @@ struct DecT {
 static_assert(HD_HUFF_LUT_BITS == 14, "primary lookup");
 typedef DecT<HD_HUFF_LUT_BITS> DecTables;
 
+// (threads below `first` only meet the barriers: they may do other work,
+// e.g. the item decoder's range search, while the rest stage)
 template <int LB>
-__device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads) {
+__device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads, uint32_t first = 0) {
   static_assert(LB == 13 || LB == 14, "lookup widths generated");
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x - first;  // (wraps above nthreads for threads below first)
+  nthreads -= first;
   const uint32_t *lut = LB == 13 ? dev::hd_huff_lut13 : dev::hd_huff_lut;
   const uint32_t *lut2 = LB == 13 ? dev::hd_huff_lut2_13 : dev::hd_huff_lut2;
   for (uint32_t i = t; i < (1u << LB); i += nthreads) T.lut[i] = lut[i];
@@ -1337,6 +1340,21 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_IW40
 #define DD_IW40 16
 #endif
+#ifndef DD_TS64
+#define DD_TS64 64u  // strings per task unit of the 64-byte instance
+#endif
+#ifndef DD_TK64
+#define DD_TK64 1u
+#endif
+#ifndef DD_TS40
+#define DD_TS40 32u  // strings per task unit of the 40-byte instance
+#endif
+#ifndef DD_TK40
+#define DD_TK40 2u  // units per task (the workgroup's last ones: one unit)
+#endif
+#ifndef DD_TAILU
+#define DD_TAILU 2u  // the workgroup's last DD_TAILU x waves units are claimed singly
+#endif
 #ifndef DD_SK40
 #define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)
 #endif
@@ -1368,7 +1386,8 @@ struct DIShared {  // k_decode_items
   alignas(16) uint32_t ob[IW][(di_obb(IP, BI) / 4 + 1 + 3) & ~3u];
   uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
-  uint32_t claimed;               // tasks of the workgroup's range claimed so far
+  uint32_t claimed, claimed1;     // tasks / tail units of the workgroup's range claimed so far
+  uint32_t range[2];              // the workgroup's task range (wave 0's search)
 };
 
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
@@ -1653,7 +1672,8 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
-template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1, uint32_t TS = TASK_STR,
+          uint32_t TK = 1>
 __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
                                                         const uint32_t *__restrict__ off,
                                                         uint32_t n, uint8_t *__restrict__ dst,
@@ -1671,10 +1691,14 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
   lds_u32 *ost = (lds_u32 *)S.ostart[wv];
-  if (threadIdx.x == 0) S.claimed = 0u;
-  stage_dec_tables(S.T, (WAVE * IW));  // the kernel's only workgroup barrier
+  if (threadIdx.x == 0) {
+    S.claimed = 0u;
+    S.claimed1 = 0u;
+  }
   const uint32_t off0 = off[0];
-  const uint32_t ntask = (n + TASK_STR - 1u) / TASK_STR;
+  // units of TS strings; the workgroup ranges are cut in tasks of TK units
+  const uint32_t ntask = (n + TS - 1u) / TS;
+  const uint32_t nrange = (n + TS * TK - 1u) / (TS * TK);
   // this workgroup's tasks: with 40-byte pieces (long values, whose tasks
   // differ several-fold in work) a contiguous range balanced by weight
   // (encoded bytes + DD_TASK_W per string) over the grid, its waves striding
@@ -1685,44 +1709,89 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   {
     const uint32_t nwg = gridDim.x, g = blockIdx.x;
     const uint64_t wtot = (uint64_t)(off[n] - off0) + (uint64_t)DD_TASK_W * n;
-    auto first_at = [&](uint64_t target) -> uint32_t {  // smallest t with weight(t) >= target
-      if (target == 0) return 0u;
-      uint32_t lo = 0, hi = ntask;  // weight(lo) < target <= weight(hi)
-      while (hi - lo > 1u) {
-        const uint32_t step = (hi - lo + WAVE - 1u) / WAVE;
-        const uint32_t c = min(lo + (lane + 1u) * step, hi);
-        const uint32_t sc = min(c * (uint32_t)TASK_STR, n);
-        const uint64_t wc = (uint64_t)(off[sc] - off0) + (uint64_t)DD_TASK_W * sc;
-        const uint64_t ge = __ballot(wc >= target);  // (lane 63 or the clamp reaches hi)
-        const uint32_t j = ge ? (uint32_t)__builtin_ctzll(ge) : WAVE - 1u;
-        const uint32_t nhi = __builtin_amdgcn_readlane(c, j);
-        lo = j ? __builtin_amdgcn_readlane(c, j - 1u) : lo;
-        hi = nhi;
+    // smallest t with weight(t) >= target, for two targets at once (the two
+    // 64-ary searches' dependent loads in flight together)
+    auto first_at2 = [&](uint64_t ta, uint64_t tb, uint32_t &ra, uint32_t &rb) {
+      uint32_t lo_a = 0, hi_a = ta ? nrange : 0u;  // weight(lo) < target <= weight(hi)
+      uint32_t lo_b = 0, hi_b = tb ? nrange : 0u;
+      while (hi_a - lo_a > 1u || hi_b - lo_b > 1u) {
+        const uint32_t st_a = (hi_a - lo_a + WAVE - 1u) / WAVE, st_b = (hi_b - lo_b + WAVE - 1u) / WAVE;
+        const uint32_t c_a = min(lo_a + (lane + 1u) * st_a, hi_a), c_b = min(lo_b + (lane + 1u) * st_b, hi_b);
+        const uint32_t s_a = min(c_a * (TS * TK), n), s_b = min(c_b * (TS * TK), n);
+        const uint32_t o_a = off[s_a], o_b = off[s_b];
+        const uint64_t w_a = (uint64_t)(o_a - off0) + (uint64_t)DD_TASK_W * s_a;
+        const uint64_t w_b = (uint64_t)(o_b - off0) + (uint64_t)DD_TASK_W * s_b;
+        if (hi_a - lo_a > 1u) {
+          const uint64_t ge = __ballot(w_a >= ta);  // (lane 63 or the clamp reaches hi)
+          const uint32_t j = ge ? (uint32_t)__builtin_ctzll(ge) : WAVE - 1u;
+          const uint32_t nhi = __builtin_amdgcn_readlane(c_a, j);
+          lo_a = j ? __builtin_amdgcn_readlane(c_a, j - 1u) : lo_a;
+          hi_a = nhi;
+        }
+        if (hi_b - lo_b > 1u) {
+          const uint64_t ge = __ballot(w_b >= tb);
+          const uint32_t j = ge ? (uint32_t)__builtin_ctzll(ge) : WAVE - 1u;
+          const uint32_t nhi = __builtin_amdgcn_readlane(c_b, j);
+          lo_b = j ? __builtin_amdgcn_readlane(c_b, j - 1u) : lo_b;
+          hi_b = nhi;
+        }
       }
-      return hi;
+      ra = hi_a;
+      rb = hi_b;
     };
-    // contiguous workgroup ranges (by weight or by count)
-    t_lo = kBal ? first_at(wtot * g / nwg) : (uint32_t)((uint64_t)ntask * g / nwg);
-    t_hi = g + 1u == nwg ? ntask
-                         : kBal ? first_at(wtot * (g + 1u) / nwg)
-                                : (uint32_t)((uint64_t)ntask * (g + 1u) / nwg);
+    // contiguous workgroup ranges (by weight or by count); the weight
+    // search runs in wave 0 while the other waves stage the tables
+    if (kBal) {
+      if (wv == 0) {
+        first_at2(wtot * g / nwg, g + 1u == nwg ? 0u : wtot * (g + 1u) / nwg, t_lo, t_hi);
+        if (g + 1u == nwg) t_hi = nrange;
+        if (lane == 0) {
+          S.range[0] = t_lo;
+          S.range[1] = t_hi;
+        }
+      }
+      stage_dec_tables(S.T, (WAVE * IW), WAVE);  // the kernel's only workgroup barriers
+      t_lo = S.range[0];
+      t_hi = S.range[1];
+    } else {
+      stage_dec_tables(S.T, (WAVE * IW));
+      t_lo = (uint32_t)((uint64_t)nrange * g / nwg);
+      t_hi = g + 1u == nwg ? nrange : (uint32_t)((uint64_t)nrange * (g + 1u) / nwg);
+    }
+    // in units (a range boundary is a task boundary: tasks of TK units stay
+    // aligned to TS * TK strings)
+    t_lo = min(t_lo * TK, ntask);
+    t_hi = min(t_hi * TK, ntask);
   }
-  // a wave's first task is t_lo + wv, later ones are claimed from the
-  // workgroup's LDS counter one task ahead (so the waves of a CU finish
-  // within a task of each other)
-  const uint32_t t_first = t_lo + wv;
+  // Tasks are runs of TK units of TS strings, claimed from the workgroup's
+  // LDS counters one task ahead (so the waves of a CU finish within a task
+  // of each other): whole tasks (aligned to TS * TK strings) from the range's
+  // front, and, TK > 1, single units from its last DD_TAILU x IW units, so
+  // that the CU's waves finish within a unit, not a whole task, of each other
+  // (round 4, config 3 decode -4 %).
+  const uint32_t t_mid = TK > 1u ? max(t_lo, t_hi > t_lo + DD_TAILU * IW
+                                                  ? t_lo + ((t_hi - t_lo - DD_TAILU * IW) / TK) * TK
+                                                  : t_lo)
+                                 : t_hi;
+  uint32_t next_k = 0;
   auto claim_next = [&](uint32_t) -> uint32_t {
-    uint32_t v = 0;
-    if (lane == 0) v = atomicAdd((uint32_t *)&S.claimed, 1u);
-    return t_lo + IW + __builtin_amdgcn_readfirstlane(v);
+    uint32_t t = 0;
+    if (lane == 0) {
+      const uint32_t v = atomicAdd((uint32_t *)&S.claimed, 1u);
+      t = t_lo + TK * v;
+      if (TK > 1u && t + TK > t_mid) t = t_mid + atomicAdd((uint32_t *)&S.claimed1, 1u);
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    next_k = t < t_hi ? (t < t_mid ? TK : 1u) : 0u;
+    return t;
   };
   // a task's string offsets are loaded one task ahead, and the first round
   // of the next task is staged into registers during the current task's
   // last round (pf), so neither waits at a task start
   uint32_t na_l = 0, nb_l = 0;
-  auto load_offs = [&](uint32_t tk, uint32_t &xa, uint32_t &xb) {
-    const uint32_t u0 = tk * TASK_STR;
-    const bool in = tk < ntask && lane < min(n - u0, (uint32_t)TASK_STR);
+  auto load_offs = [&](uint32_t tk, uint32_t kk, uint32_t &xa, uint32_t &xb) {
+    const uint32_t u0 = tk * TS;
+    const bool in = tk < ntask && lane < min(n - u0, TS * kk);
     xa = in ? off[u0 + lane] : 0u;
     xb = in ? off[u0 + lane + 1] : 0u;
   };
@@ -1736,17 +1805,19 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   };
   uint4 pf[kPF];
   uint32_t pf_IB = 0xFFFFFFFFu;
-  load_offs(t_first < t_hi ? t_first : ntask, na_l, nb_l);
+  const uint32_t t_first = claim_next(0u);
+  uint32_t task_k = next_k;
+  load_offs(t_first < t_hi ? t_first : ntask, task_k, na_l, nb_l);
   uint32_t next_task = t_hi;
   for (uint32_t task = t_first; task < t_hi;) {
     next_task = claim_next(task);
-    const uint32_t t0 = task * TASK_STR;
-    const uint32_t nstr = min(n - t0, (uint32_t)TASK_STR);
+    const uint32_t t0 = task * TS;
+    const uint32_t nstr = min(n - t0, TS * task_k);
     const bool sl = lane < nstr;
     const uint32_t a_l = na_l, b_l = nb_l;
     const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
     const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
-    load_offs(next_task < t_hi ? next_task : ntask, na_l, nb_l);
+    load_offs(next_task < t_hi ? next_task : ntask, next_k, na_l, nb_l);
     const uint64_t tbase = auto_slot(A - off0, t0);
     const bool task_ovf = auto_slot(Z - off0, t0 + nstr) > dst_cap;
     if (__ballot(sl && (b_l < a_l || a_l < off0))) {
@@ -1758,6 +1829,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase, dst_cap);
       }
       task = next_task;
+      task_k = next_k;
       continue;
     }
     // items: m_l of string l, X_l the first
@@ -1848,7 +1920,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         } else if (next_task < t_hi) {
           const uint32_t An = __builtin_amdgcn_readfirstlane(na_l);
           const uint32_t Zn = __builtin_amdgcn_readlane(
-              nb_l, min(n - next_task * TASK_STR, (uint32_t)TASK_STR) - 1u);
+              nb_l, min(n - next_task * TS, TS * next_k) - 1u);
           round_range(An, An, Zn, IBn, ncn);
           pf_IB = IBn;
         }
@@ -2007,6 +2079,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     task = next_task;
+    task_k = next_k;
   }
 }
 
@@ -2124,13 +2197,15 @@ static int hip_rv(hipError_t e) {
 }
 
 #ifndef HD_PART_ENC
-template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1>
+template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1, uint32_t TS = TASK_STR,
+          uint32_t TK = 1>
 static void launch_decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
                                 uint8_t *dst, size_t dst_cap, uint32_t *dst_off,
                                 int32_t *status, uint16_t *fstate, uint8_t *flags,
                                 hipStream_t st) {
-  hipLaunchKernelGGL((k_decode_items<IP, IW, LB, BI, SK>),
-                     dim3(persistent_grid<k_decode_items<IP, IW, LB, BI, SK>, WAVE * IW, TASK_STR * IW>(n)),
+  static_assert(TS >= 1 && TS * TK <= TASK_STR, "a task's strings map to lanes");
+  hipLaunchKernelGGL((k_decode_items<IP, IW, LB, BI, SK, TS, TK>),
+                     dim3(persistent_grid<k_decode_items<IP, IW, LB, BI, SK, TS, TK>, WAVE * IW, TS * TK * IW>(n)),
                      dim3(WAVE * IW), 0, st, src, src_off, n, dst, (uint64_t)dst_cap, dst_off,
                      status, fstate, flags);
 }
@@ -2159,9 +2234,9 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
   if (enc_bytes <= 48ull * n)
-    launch_decode_items<64u, DD_IW64, 13, DD_BI64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<64u, DD_IW64, 13, DD_BI64, 1u, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
-    launch_decode_items<40u, DD_IW40, 13, DD_BI40, DD_SK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<40u, DD_IW40, 13, DD_BI40, DD_SK40, DD_TS40, DD_TK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
 }
 

@@ -261,8 +261,8 @@ class HuffmanBatchCodec:
     def decode_auto(self, src, src_off, enc_bytes=None, dst=None, dst_off=None, status=None,
                     want_ctx=False, stream=None, pick=None):
         """Decode into a dense pool (one launch): the strings of each task of
-        64 consecutive strings back to back from the task's base
-        auto_slot(x_t0, t0).  enc_bytes = src_off[n] - src_off[0] sizes dst and
+        64 consecutive strings (or of a task split into two of 32) back to
+        back from the task's base auto_slot(x_t0, t0).  enc_bytes = src_off[n] - src_off[0] sizes dst and
         picks the kernel instance by the mean string length; when it is not
         given it is read from src_off on the call's stream (a host
         synchronisation of that stream: pass it to keep the call

@@ -90,7 +90,13 @@ for cfg in [int(c) for c in sys.argv[1:]] or [3, 2, 5]:
             dec(k)
         torch.cuda.synchronize()
         used = int(doff[-1].item()) & 0xFFFFFFFF
-        cur = (dst[:used].clone(), doff.clone(), st.clone(), fs.clone(), fl.clone())
+        # each string's bytes gathered through the library's own offsets (the
+        # offsets and the gaps between tasks' outputs move with the task
+        # decomposition; status, state and bytes may not)
+        w = torch.clamp(st, min=0).long()
+        starts = torch.repeat_interleave(doff[:n].long() & 0xFFFFFFFF, w)
+        rel = torch.arange(int(w.sum().item()), device=dev) - torch.repeat_interleave(torch.cumsum(w, 0) - w, w)
+        cur = (dst[starts + rel].clone(), st.clone(), fs.clone(), fl.clone())
         if ref is None:
             ref = cur
         same[k] = all(torch.equal(x, y) for x, y in zip(ref, cur))
