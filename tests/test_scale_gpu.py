@@ -278,6 +278,37 @@ def test_encode_wave_output_near_2_32_bits(codec, dev):
     torch.cuda.empty_cache()
 
 
+def test_encode_dst_cap_below_bound_guard(codec, dev):
+    """A pool smaller than the encoded batch (dst_cap below encode_bound and
+    below the output itself, not a multiple of 16): the tiles that fit are
+    exact, the first one that does not and every later one write nothing
+    (saturated offsets, the overflow mark), and no byte at or past dst_cap
+    is written (guard bytes intact)."""
+    import torch
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_mixed_values(40000, seed=77)
+    renc, reoff = O.encode_batch(pool, off, nthreads=8)
+    E = int(reoff[-1])
+    cap = (E * 3) // 5 + 7
+    dst = torch.full((cap + 8192,), 0xAB, dtype=torch.uint8, device=dev)
+    eoff = torch.empty(len(off), dtype=torch.int32, device=dev)
+    src = to_dev(np.concatenate([pool, np.zeros(16, np.uint8)]), dev)
+    codec.encode(src, to_dev(off, dev), raw_bytes=int(off[-1]), dst=dst[:cap], dst_off=eoff)
+    torch.cuda.synchronize()
+    eo = _u32(eoff).astype(np.int64)
+    assert eo[-1] == 0xFFFFFFFF, "overflow mark"
+    assert bool((dst[cap:] == 0xAB).all()), "a byte at or past dst_cap was written"
+    # the strings whose tile fits: offsets and bytes equal the oracle's
+    ok = np.nonzero(reoff[1:].astype(np.int64) <= cap)[0]
+    fits = ok[ok < (len(ok) // 256) * 256]  # whole tiles before the cut
+    assert fits.size > 0
+    k = int(fits[-1]) + 1
+    assert np.array_equal(eo[:k], reoff[:k].astype(np.int64))
+    d = dst[:int(reoff[k])].cpu().numpy()
+    assert np.array_equal(d, renc[:int(reoff[k])])
+    assert (eo[k:-1] <= cap).all(), "offsets saturate at dst_cap"
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
