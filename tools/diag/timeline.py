@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave timeline of the item decoder (a DD_TIMELINE build,
-tools/diag/lib_tl.so): s_memrealtime (100 MHz) at entry, after the range
+tools/diag/lib_tl.so from
+`PATCH=tools/diag/patches/r4_diag_hooks.patch build_variants.sh tl:-DDD_TIMELINE`): s_memrealtime (100 MHz) at entry, after the range
 search + table staging, after each task, at exit.  Prints the launch span,
 the startup share and how far apart waves and workgroups finish."""
 import ctypes, os, sys, json
