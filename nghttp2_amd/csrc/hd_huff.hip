@@ -1390,6 +1390,7 @@ struct DIShared {  // k_decode_items
   uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
   uint32_t claimed, claimed1;     // tasks / tail units of the workgroup's range claimed so far
   uint32_t range[2];              // the workgroup's task range (wave 0's search)
+  uint8_t tperm[64];              // claim order of the range's tail units (largest first)
 };
 
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
@@ -1674,6 +1675,45 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
 // (status), a plain scan of the lanes' byte counts places the regions back
 // to back from the task's base, and each lane stores its bytes.
 // ---------------------------------------------------------------------------
+// The claim order of a workgroup range's tail units (k_decode_items, TK > 1):
+// largest first by items (ceil(E / IP) per string), so that the units claimed
+// last, whose end is the workgroup's, are the short ones.  One wave, before
+// the workgroup barrier: the range's last DD_TAILU x IW units (<= 64, <= 64 x
+// TS strings) are read as offsets, their items summed per unit, ranked.
+// (t_lo / t_hi in ranges of TK units, as the search returns them.)
+template <uint32_t IP, uint32_t TS, uint32_t TK, int IW>
+__device__ __forceinline__ void dd_tail_order(const uint32_t *__restrict__ off, uint32_t n,
+                                              uint32_t ntask, uint32_t r_lo, uint32_t r_hi,
+                                              uint8_t *tperm, uint32_t lane) {
+  static_assert(TS == 32u && DD_TAILU * IW <= 64, "tail units: 32 strings, two per 64 lanes");
+  const uint32_t u_lo = min(r_lo * TK, ntask), u_hi = min(r_hi * TK, ntask);
+  const uint32_t t_mid = max(u_lo, u_hi > u_lo + DD_TAILU * IW
+                                       ? u_lo + ((u_hi - u_lo - DD_TAILU * IW) / TK) * TK
+                                       : u_lo);
+  const uint32_t nt = u_hi - t_mid;  // <= DD_TAILU * IW + TK - 1
+  if (nt == 0u) return;
+  const uint32_t s0 = t_mid * TS, s1 = min(u_hi * TS, n);
+  uint32_t cu = 0;  // lane u: unit u's items
+  for (uint32_t j = 0; j < (nt + 1u) / 2u; ++j) {  // units 2j (lanes 0-31), 2j+1 (32-63)
+    const uint32_t s = s0 + 64u * j + lane;
+    uint32_t it = 0;
+    if (s < s1) {
+      const uint32_t e = off[s + 1] - off[s];
+      it = e > IP ? (e + IP - 1u) / IP : 1u;
+    }
+    const uint32_t inc = wave_incl_scan(it);
+    const uint32_t lo = __builtin_amdgcn_readlane(inc, 31), all = __builtin_amdgcn_readlane(inc, 63);
+    cu = lane == 2u * j ? lo : lane == 2u * j + 1u ? all - lo : cu;
+  }
+  // rank: larger first, ties by index
+  uint32_t rank = 0;
+  for (uint32_t v = 0; v < nt; ++v) {
+    const uint32_t cv = __builtin_amdgcn_readlane(cu, v);
+    rank += (cv > cu || (cv == cu && v < lane)) ? 1u : 0u;
+  }
+  if (lane < nt) tperm[rank] = (uint8_t)lane;
+}
+
 template <uint32_t IP, int IW, int LB, uint32_t BI = 0, uint32_t SK = 1, uint32_t TS = TASK_STR,
           uint32_t TK = 1>
 __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__restrict__ src,
@@ -1751,6 +1791,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           S.range[0] = t_lo;
           S.range[1] = t_hi;
         }
+        if constexpr (TK > 1u) dd_tail_order<IP, TS, TK, IW>(off, n, ntask, t_lo, t_hi, S.tperm, lane);
       }
       stage_dec_tables(S.T, (WAVE * IW), WAVE);  // the kernel's only workgroup barriers
       t_lo = S.range[0];
@@ -1781,7 +1822,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     if (lane == 0) {
       const uint32_t v = atomicAdd((uint32_t *)&S.claimed, 1u);
       t = t_lo + TK * v;
-      if (TK > 1u && t + TK > t_mid) t = t_mid + atomicAdd((uint32_t *)&S.claimed1, 1u);
+      if (TK > 1u && t + TK > t_mid) {
+        const uint32_t c = atomicAdd((uint32_t *)&S.claimed1, 1u);
+        t = t_mid + (kBal && c < t_hi - t_mid ? (uint32_t)S.tperm[c] : c);
+      }
     }
     t = __builtin_amdgcn_readfirstlane(t);
     next_k = t < t_hi ? (t < t_mid ? TK : 1u) : 0u;

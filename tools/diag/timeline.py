@@ -56,3 +56,9 @@ for m in [int(x) for x in (sys.argv[1:] or ["1"])]:
                     "wg_end_min_med_max": [round(float(x), 1) for x in (wg_end.min(), np.median(wg_end), wg_end.max())],
                     "in_wg_spread_med_us": round(float(np.median(wg_end - wg_first_end)), 1)})
     print(json.dumps({"strings_M": m, "runs": res[1:]}), flush=True)
+    # the last run's per-workgroup end times and its waves' first-task ends
+    # (for correlating with the workgroup's work, computed on the host)
+    print(json.dumps({"strings_M": m, "wg_end_us": [round(float(x), 2) for x in wg_end],
+                      "wg_start_us": [round(float(ts[wg == g, 0].min()), 2) for g in range(wg.max() + 1)]}),
+          flush=True)
+    np.save(os.path.join(os.environ.get("TL_OUT", "."), "eoff_%dM.npy" % m), eo.cpu().numpy())
