@@ -53,8 +53,8 @@ CPU_SAMPLE = 1 << 20  # strings of the cpu_baseline sample (bounded CPU work)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
                     help="default: 3 on one GPU, 4 (16M sharded) on more")
     ap.add_argument("--strings", type=int, default=None,
