@@ -1391,6 +1391,7 @@ struct DIShared {  // k_decode_items
   uint32_t claimed, claimed1;     // tasks / tail units of the workgroup's range claimed so far
   uint32_t range[2];              // the workgroup's task range (wave 0's search)
   uint8_t tperm[64];              // claim order of the range's tail units (largest first)
+  uint32_t tready;                // tperm written (wave 0, after the barrier)
 };
 
 struct DiscardSink {  // a warm-up: its symbols belong to the item before
@@ -1677,10 +1678,11 @@ __device__ __forceinline__ void dd_finish(const TT &T, bool failed, uint32_t t,
 // ---------------------------------------------------------------------------
 // The claim order of a workgroup range's tail units (k_decode_items, TK > 1):
 // largest first by items (ceil(E / IP) per string), so that the units claimed
-// last, whose end is the workgroup's, are the short ones.  One wave, before
-// the workgroup barrier: the range's last DD_TAILU x IW units (<= 64, <= 64 x
-// TS strings) are read as offsets, their items summed per unit, ranked.
-// (t_lo / t_hi in ranges of TK units, as the search returns them.)
+// last, whose end is the workgroup's, are the short ones.  Wave 0, after the
+// workgroup barrier while the other waves decode (before it, every wave
+// waited ~5.5 us for it): the range's last DD_TAILU x IW units (<= 64, <= 64
+// x TS strings) are read as offsets, their items summed per unit, ranked.
+// (r_lo / r_hi in ranges of TK units, as the search returns them.)
 template <uint32_t IP, uint32_t TS, uint32_t TK, int IW>
 __device__ __forceinline__ void dd_tail_order(const uint32_t *__restrict__ off, uint32_t n,
                                               uint32_t ntask, uint32_t r_lo, uint32_t r_hi,
@@ -1736,6 +1738,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   if (threadIdx.x == 0) {
     S.claimed = 0u;
     S.claimed1 = 0u;
+    S.tready = 0u;
   }
   const uint32_t off0 = off[0];
   // units of TS strings; the workgroup ranges are cut in tasks of TK units
@@ -1791,11 +1794,19 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           S.range[0] = t_lo;
           S.range[1] = t_hi;
         }
-        if constexpr (TK > 1u) dd_tail_order<IP, TS, TK, IW>(off, n, ntask, t_lo, t_hi, S.tperm, lane);
       }
       stage_dec_tables(S.T, (WAVE * IW), WAVE);  // the kernel's only workgroup barriers
       t_lo = S.range[0];
       t_hi = S.range[1];
+      // the tail's claim order: wave 0, after the barrier (the others start
+      // decoding); a tail claim waits for it (in practice it is long ready)
+      if constexpr (TK > 1u) {
+        if (wv == 0) {
+          dd_tail_order<IP, TS, TK, IW>(off, n, ntask, t_lo, t_hi, S.tperm, lane);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store((uint32_t *)&S.tready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
     } else {
       stage_dec_tables(S.T, (WAVE * IW));
       t_lo = (uint32_t)((uint64_t)nrange * g / nwg);
@@ -1824,7 +1835,14 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       t = t_lo + TK * v;
       if (TK > 1u && t + TK > t_mid) {
         const uint32_t c = atomicAdd((uint32_t *)&S.claimed1, 1u);
-        t = t_mid + (kBal && c < t_hi - t_mid ? (uint32_t)S.tperm[c] : c);
+        if (kBal && c < t_hi - t_mid) {
+          while (__hip_atomic_load((uint32_t *)&S.tready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+            __builtin_amdgcn_s_sleep(4);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          t = t_mid + (uint32_t)S.tperm[c];
+        } else {
+          t = t_mid + c;
+        }
       }
     }
     t = __builtin_amdgcn_readfirstlane(t);
