@@ -1324,8 +1324,10 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 // ---------------------------------------------------------------------------
 // decode_batch_auto: the item decoder and its helpers
 // ---------------------------------------------------------------------------
+#ifndef DD_OV
 #define DD_OV 20u  // warm-up bytes of a later item (round 2, 24: 314.2 vs 306.5 us on config 3;
                    // round 3 with overshooting warm-ups, 16/18/22: 312.4/308.9/304.8 vs 300.8)
+#endif
 #ifndef DD_TASK_W
 #define DD_TASK_W 32u  // a string's weight in bytes when balancing tasks over workgroups
 #endif
