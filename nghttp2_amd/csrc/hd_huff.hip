@@ -425,6 +425,35 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
 // ends bytewise), the partial last word carried into the next round.  The
 // first chunk's bytes before A are placed before the wave's first bit, in
 // a margin of the image that is never stored.
+// The tile sums' exclusive 64-bit prefix for a large batch (one workgroup):
+// past EC_SCAN_TILES tiles, k_encode's own sum of the tiles before it (each
+// workgroup reads all of them, O(tiles^2) L2 reads: 8.6 GB for 16M strings)
+// costs more than this launch.  A poisoned tile (0xFFFFFFFF) pushes every
+// later prefix past the uint32 offsets, as the in-kernel sum does.
+#define EC_SCAN_TILES 16384u
+__global__ __launch_bounds__(1024) void k_tile_prefix64(const uint32_t *__restrict__ tiles, uint32_t nt,
+                                                        uint64_t *__restrict__ pre) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t per = (nt + 1023u) / 1024u, b = min(t * per, nt), e = min(b + per, nt);
+  uint64_t s = 0;
+  for (uint32_t i = b; i < e; ++i) s += tiles[i];
+  uint64_t inc = s;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint64_t v = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63u) wsum[wv] = inc;
+  __syncthreads();
+  uint64_t run = inc - s;
+  for (uint32_t w = 0; w < wv; ++w) run += wsum[w];
+  for (uint32_t i = b; i < e; ++i) {
+    pre[i] = run;
+    run += tiles[i];
+  }
+}
+
 #ifndef EC_WPE
 #define EC_WPE 4  // k_encode: waves per SIMD the register budget is sized for
 #endif
@@ -458,7 +487,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
                                                uint32_t *__restrict__ dst_off,
-                                               const uint32_t *__restrict__ tile_sums) {
+                                               const uint32_t *__restrict__ tile_sums,
+                                               const uint64_t *__restrict__ tile_pre) {
   constexpr uint32_t RW = FR ? EC_RW_F : EC_RW;
   constexpr uint32_t PDW = FR ? 512u : 256u;  // u16 extras / u8 pads per round byte
   __shared__ uint2 codeT[256];  // {code MSB-aligned, length}
@@ -499,7 +529,10 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   // strings, L2-resident), summed with independent loads in flight, in 64
   // bits (a batch's encoded total may pass the uint32 offset range)
   uint64_t pre = 0;
-  {
+  if (tile_pre) {  // a large batch: the prefixes were scanned by k_tile_prefix64
+    // (pre is each thread's part of the sum the block scans add up)
+    pre = threadIdx.x == 0 ? tile_pre[blockIdx.x] : 0u;
+  } else {
     uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t t = threadIdx.x;
     for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
@@ -2335,8 +2368,18 @@ size_t nghttp2_amd_hd_huff_decode_bound(uint64_t enc_bytes, uint32_t n) {
   return (size_t)((b + 15u) & ~(uint64_t)15u);
 }
 
+// the tile sums, then (8-aligned) their 64-bit prefixes for a large batch
+static size_t ws_pre_offset(uint32_t nt) { return (((size_t)nt + 16u) * sizeof(uint32_t) + 7u) & ~(size_t)7u; }
 size_t nghttp2_amd_hd_huff_workspace_size(uint32_t n) {
-  return ((size_t)ntiles_for(n) + 16u) * sizeof(uint32_t);
+  const uint32_t nt = ntiles_for(n);
+  return ws_pre_offset(nt) + (nt > EC_SCAN_TILES ? (size_t)nt * sizeof(uint64_t) : 0u);
+}
+// k_encode's tile prefixes: scanned in their own launch for a large batch
+static const uint64_t *scan_tile_prefix(const uint32_t *tiles, uint32_t nt, void *workspace, hipStream_t st) {
+  if (nt <= EC_SCAN_TILES || ((uintptr_t)workspace & 7u)) return nullptr;
+  uint64_t *pre = (uint64_t *)((char *)workspace + ws_pre_offset(nt));
+  hipLaunchKernelGGL(k_tile_prefix64, dim3(1), dim3(1024), 0, st, tiles, nt, pre);
+  return pre;
 }
 
 size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw_bytes, uint32_t n) {
@@ -2366,8 +2409,9 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
   hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
+  const uint64_t *pre = scan_tile_prefix(tiles, nt, workspace, st);
   hipLaunchKernelGGL(k_encode<false>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, pre);
   return hip_rv(hipGetLastError());
 }
 
@@ -2401,8 +2445,9 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
   const uint32_t nt = ntiles_for(n);
   uint32_t *tiles = (uint32_t *)workspace;
   hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
+  const uint64_t *pre = scan_tile_prefix(tiles, nt, workspace, st);
   hipLaunchKernelGGL(k_encode<true>, dim3(nt), dim3(WG), 0, st, src, src_off, n, dst,
-                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles);
+                     (uint64_t)dst_cap, dst_off, (const uint32_t *)tiles, pre);
   return hip_rv(hipGetLastError());
 }
 

@@ -278,6 +278,30 @@ def test_encode_wave_output_near_2_32_bits(codec, dev):
     torch.cuda.empty_cache()
 
 
+def test_encode_large_batch_scanned_tile_prefix(codec, dev):
+    """Past 16,384 tiles of 256 strings the tile prefixes are scanned in their
+    own launch (k_tile_prefix64) instead of summed by every k_encode
+    workgroup: 4.5M config-2 strings (17,579 tiles), offsets and encoded
+    bytes bit-exact against the oracle (emit_strings takes the same path)."""
+    import hashlib
+    import torch
+    from nghttp2_amd import workloads as W
+    n = 4_500_000
+    pool, off = W.gen_pseudo_headers(n, seed=0x5CA9)
+    assert (n + 255) // 256 > 16384
+    renc, reoff = O.encode_batch(pool, off, nthreads=16)
+    src = to_dev(np.concatenate([pool, np.zeros(16, np.uint8)]), dev)
+    so = to_dev(off, dev)
+    enc, eoff = codec.encode(src, so, raw_bytes=int(off[-1]))
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(eoff), reoff.astype(np.uint32)), "offsets"
+    E = int(reoff[-1])
+    assert hashlib.sha256(enc[:E].cpu().numpy().tobytes()).digest() == \
+        hashlib.sha256(renc[:E].tobytes()).digest(), "encoded bytes"
+    del enc, eoff
+    torch.cuda.empty_cache()
+
+
 def test_encode_dst_cap_below_bound_guard(codec, dev):
     """A pool smaller than the encoded batch (dst_cap below encode_bound and
     below the output itself, not a multiple of 16): the tiles that fit are
