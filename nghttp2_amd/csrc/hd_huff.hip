@@ -430,7 +430,9 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
 // workgroup reads all of them, O(tiles^2) L2 reads: 8.6 GB for 16M strings)
 // costs more than this launch.  A poisoned tile (0xFFFFFFFF) pushes every
 // later prefix past the uint32 offsets, as the in-kernel sum does.
+#ifndef EC_SCAN_TILES
 #define EC_SCAN_TILES 16384u
+#endif
 __global__ __launch_bounds__(1024) void k_tile_prefix64(const uint32_t *__restrict__ tiles, uint32_t nt,
                                                         uint64_t *__restrict__ pre) {
   __shared__ uint64_t wsum[16];
