@@ -319,3 +319,99 @@ def name_tokens(names):
     """(token[], hash[]) for a list of names: what
     nghttp2_amd_hd_name_tokens_batch returns."""
     return [lookup_token(n) for n in names], [name_hash(n) for n in names]
+
+
+# ---------------------------------------------------------------------------
+# The same inflater in C (oracle/hpack_inflate_oracle.c): checked against the
+# Python Inflater above (tests/test_inflate_c_oracle.py) and timed as the
+# inflate front-end's CPU baseline (tools/bench_rows.py).
+# ---------------------------------------------------------------------------
+def _clib():
+    import ctypes
+    L = O.lib()
+    if not getattr(L, "_ohi_bound", False):
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.ohi_new.restype = vp
+        L.ohi_del.argtypes = [vp]
+        L.ohi_change_table_size.argtypes = [vp, sz]
+        L.ohi_num_entries.restype = sz
+        L.ohi_num_entries.argtypes = [vp]
+        L.ohi_table_size.restype = sz
+        L.ohi_table_size.argtypes = [vp]
+        L.ohi_get_entry.argtypes = [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz),
+                                    ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.ohi_inflate_block.restype = ctypes.c_long
+        L.ohi_inflate_block.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), vp, sz,
+                                        ctypes.POINTER(sz)]
+        L.ohi_inflate_batch_timed.restype = ctypes.c_double
+        L.ohi_inflate_batch_timed.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_int, ctypes.POINTER(ctypes.c_long)]
+        L._ohi_bound = True
+    return L
+
+
+class CInflater:
+    """oracle/hpack_inflate_oracle.c behind the Inflater interface."""
+
+    def __init__(self):
+        self.L = _clib()
+        self.p = self.L.ohi_new()
+        assert self.p
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.ohi_del(self.p)
+            self.p = None
+
+    def change_table_size(self, v):
+        self.L.ohi_change_table_size(self.p, v)
+
+    @property
+    def table(self):
+        import ctypes
+        out = []
+        for k in range(self.L.ohi_num_entries(self.p)):
+            n, v = ctypes.c_void_p(), ctypes.c_void_p()
+            nl, vl = ctypes.c_size_t(), ctypes.c_size_t()
+            self.L.ohi_get_entry(self.p, k, ctypes.byref(n), ctypes.byref(nl), ctypes.byref(v),
+                                 ctypes.byref(vl))
+            out.append((ctypes.string_at(n, nl.value) if nl.value else b"",
+                        ctypes.string_at(v, vl.value) if vl.value else b""))
+        return out
+
+    def table_size(self):
+        return self.L.ohi_table_size(self.p)
+
+    def inflate_block(self, block):
+        import ctypes
+        b = bytes(block)
+        acap = 64 * len(b) + 8 * 4096 + 64
+        nvcap = len(b) + 16
+        arena = ctypes.create_string_buffer(acap)
+        nv = (ctypes.c_uint32 * (5 * nvcap))()
+        au, nu = ctypes.c_size_t(), ctypes.c_size_t()
+        bb = ctypes.create_string_buffer(b, max(1, len(b)))
+        rv = self.L.ohi_inflate_block(self.p, bb, len(b), arena, acap, ctypes.byref(au), nv, nvcap,
+                                      ctypes.byref(nu))
+        assert rv != -2, "buffers"
+        raw = arena.raw[:au.value]
+        fields = [(raw[nv[5 * k]:nv[5 * k] + nv[5 * k + 1]],
+                   raw[nv[5 * k + 2]:nv[5 * k + 2] + nv[5 * k + 3]], nv[5 * k + 4])
+                  for k in range(nu.value)]
+        return int(rv), fields
+
+
+def c_inflate_batch_timed(blocks, conns, nconn, nthreads):
+    """Inflate `blocks` (block i on connection conns[i]) with fresh C
+    inflaters on `nthreads` threads; returns (seconds, fields)."""
+    import ctypes
+    L = _clib()
+    m = len(blocks)
+    keep = [ctypes.create_string_buffer(bytes(b), max(1, len(b))) for b in blocks]
+    ptrs = (ctypes.c_void_p * m)(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+    lens = (ctypes.c_size_t * m)(*[len(b) for b in blocks])
+    cs = (ctypes.c_uint32 * m)(*conns)
+    nf = ctypes.c_long()
+    dt = L.ohi_inflate_batch_timed(ptrs, lens, cs, m, nconn, nthreads, ctypes.byref(nf))
+    assert dt >= 0 and nf.value >= 0
+    return dt, nf.value

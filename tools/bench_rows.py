@@ -193,7 +193,18 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5, index=False):
         assert rv == 0 and nv_used.value == nf
         best_c = t if best_c is None or t < best_c else best_c
     assert list(stc) == list(st)
-    return {"blocks": len(blocks), "connections": nconn, "fields": nf, "wire_bytes": wire,
+    # CPU baseline: the oracle's C inflater (oracle/hpack_inflate_oracle.c,
+    # the same algorithm, fresh inflaters per run) on 1 and 16 threads
+    cpu = {}
+    for t in (1, 16):
+        best = None
+        for _ in range(3):
+            dt, nfc = HO.c_inflate_batch_timed(blocks, conns, nconn, t)
+            assert nfc == nf
+            best = dt if best is None or dt < best else best
+        cpu["cpu_port_%dt_s" % t] = round(best, 5)
+        cpu["cpu_port_%dt_wire_MBps" % t] = round(wire / best / 1e6, 1)
+    return {"blocks": len(blocks), "connections": nconn, "fields": nf, "wire_bytes": wire, **cpu,
             "incremental_indexing": index,
             "c_s_per_call": round(best_c, 5), "c_wire_MBps": round(wire / best_c / 1e6, 1),
             "c_fields_per_s": round(nf / best_c),
