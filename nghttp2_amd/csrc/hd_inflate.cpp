@@ -233,6 +233,12 @@ struct Engine {
   int32_t *d_st = nullptr;
   size_t din_cap = 0, dout_cap = 0, dn_cap = 0;
   std::vector<BlockOut> outs;
+  // pass 1 state, kept across calls (under mu)
+  std::vector<Block> bl;
+  std::vector<uint32_t> nhuff;
+  std::vector<uint64_t> hbytes;
+  std::vector<const Lit *> huff;
+  std::vector<uint32_t> hoff;
 };
 Engine &engine() {
   static Engine e;
@@ -280,6 +286,7 @@ bool parse_block(const uint8_t *in, size_t len, Block &b) {
     pos += n;
     return true;
   };
+  b.ops.clear();  // (kept across calls: no allocation once grown)
   b.ops.reserve(len / 4 + 1);
   while (pos < len) {
     Op op;
@@ -514,55 +521,69 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   for (uint32_t i = 0; i < nblocks; ++i)
     if (!inflaters[i] || (!blocks[i] && block_lens[i])) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
 
-  // ---- pass 1: parse every block (stateless: one task per block)
+  // ---- pass 1: parse every block (stateless: one task per block); the
+  // engine's buffers are reused across calls, so a warm call allocates
+  // nothing here
   using nghttp2_amd_host::parallel_for;
   nghttp2_amd_host::Phases ph("inflate");
-  std::vector<Block> bl(nblocks);
-  std::vector<uint32_t> nhuff(nblocks + 1, 0);  // Huffman literals per block, then prefix
+  std::lock_guard<std::mutex> guard(engine().mu);
+  Engine &E = engine();
+  if (E.bl.size() < nblocks) E.bl.resize(nblocks);
+  E.nhuff.assign(nblocks + 1, 0);  // Huffman literals per block, then prefix
+  E.hbytes.assign(nblocks + 1, 0);  // their bytes per block, then prefix
+  std::vector<Block> &bl = E.bl;
+  std::vector<uint32_t> &nhuff = E.nhuff;
   parallel_for(nblocks, 64, [&](size_t i) {
     // a malformed block keeps the representations before the error: the
     // reference emits those fields before it fails
     bl[i].parse_ok = parse_block(blocks[i], block_lens[i], bl[i]);
     uint32_t c = 0;
+    uint64_t by = 0;
     for (const Op &op : bl[i].ops)
-      if (op.kind == Op::LITERAL) c += (op.name.huff == 0) + (op.val.huff == 0);
+      if (op.kind == Op::LITERAL) {
+        if (op.name.huff == 0) ++c, by += op.name.len;
+        if (op.val.huff == 0) ++c, by += op.val.len;
+      }
     nhuff[i + 1] = c;
+    E.hbytes[i + 1] = by;
   });
-  for (uint32_t i = 0; i < nblocks; ++i) nhuff[i + 1] += nhuff[i];
-  const uint32_t nh = nhuff[nblocks];
-  std::vector<const Lit *> huff(nh);
-  std::vector<uint32_t> hoff(nh + 1, 0);
   for (uint32_t i = 0; i < nblocks; ++i) {
+    nhuff[i + 1] += nhuff[i];
+    E.hbytes[i + 1] += E.hbytes[i];
+  }
+  const uint32_t nh = nhuff[nblocks];
+  // uint32 offsets into the batch's literal pool (and uint32 decode slots):
+  // a batch past them is refused before any connection state changes
+  if (E.hbytes[nblocks] > UINT32_MAX ||
+      (nh && nghttp2_amd_hd_huff_decode_bound(E.hbytes[nblocks], nh) > UINT32_MAX))
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (E.huff.size() < nh) E.huff.resize(nh);
+  if (E.hoff.size() < (size_t)nh + 1) E.hoff.resize((size_t)nh + 1);
+  std::vector<const Lit *> &huff = E.huff;
+  std::vector<uint32_t> &hoff = E.hoff;
+  hoff[0] = 0;
+  parallel_for(nblocks, 64, [&](size_t i) {  // each block numbers and places its literals
     uint32_t k = nhuff[i];
+    uint32_t o = (uint32_t)E.hbytes[i];
     for (Op &op : bl[i].ops) {
       if (op.kind != Op::LITERAL) continue;
       if (op.name.huff == 0) {
         op.name.huff = (int32_t)k;
-        huff[k++] = &op.name;
+        huff[k] = &op.name;
+        o += op.name.len;
+        hoff[++k] = o;
       }
       if (op.val.huff == 0) {
         op.val.huff = (int32_t)k;
-        huff[k++] = &op.val;
+        huff[k] = &op.val;
+        o += op.val.len;
+        hoff[++k] = o;
       }
     }
-  }
-  {
-    // uint32 offsets into the batch's literal pool (and uint32 decode slots):
-    // a batch past them is refused before any connection state changes
-    uint64_t tot = 0;
-    for (uint32_t k = 0; k < nh; ++k) {
-      tot += huff[k]->len;
-      if (tot > UINT32_MAX) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-      hoff[k + 1] = (uint32_t)tot;
-    }
-    if (nh && nghttp2_amd_hd_huff_decode_bound(tot, nh) > UINT32_MAX)
-      return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  }
+  });
 
   ph.mark("parse");
   // ---- GPU: every Huffman literal of the batch in one decode
-  std::lock_guard<std::mutex> guard(engine().mu);
-  Engine &E = engine();
   const uint8_t *dec = nullptr;
   const uint32_t *slot = nullptr;
   const int32_t *hst = nullptr;
