@@ -617,15 +617,16 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
         hipMemcpyAsync(h_slot, E.d_slot, (nh + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                        st) != hipSuccess ||
         hipMemcpyAsync(h_st, E.d_st, nh * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
-            hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+            hipSuccess)
       return NGHTTP2_AMD_ERR_FATAL;
     dec = E.h_pool;
     slot = h_slot;
     hst = h_st;
   }
 
-  ph.mark("gpu");
+  ph.mark("gpu issued");
+  // (the decode runs while the host groups the blocks by connection and
+  // bounds the output below; replay waits for it)
   // ---- pass 2: each connection's blocks in batch order against its table
   // (one task per connection), fields into per-block buffers
   const LitSrc ls{dec, slot, hst};
@@ -657,17 +658,25 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     // (saturating: a table limit near SIZE_MAX must not wrap the bound)
     auto sat = [](uint64_t a, uint64_t b) -> uint64_t { return a > UINT64_MAX - b ? UINT64_MAX : a + b; };
     uint64_t nv_bound = 0, ar_bound = 0;
+    // (a Huffman literal at its decode bound: the decode is still running)
     auto lit_len = [&](const Lit &l) -> uint64_t {
-      if (l.huff < 0) return l.len;
-      return hst[l.huff] >= 0 ? (uint64_t)hst[l.huff] : (uint64_t)l.len * 8u / 5u + 1u;
+      return l.huff < 0 ? (uint64_t)l.len : (uint64_t)l.len * 8u / 5u + 1u;
     };
     for (uint32_t i = 0; i < nblocks && !may_cut; ++i) {
       const uint64_t rm = std::min<uint64_t>(ref_max[conn_of[inflaters[i]]], UINT32_MAX);
+      // (a static-table reference at its entry's own length)
+      auto ref_len = [&](uint32_t idx, bool name_only) -> uint64_t {
+        if (idx >= 1 && idx <= kStaticLen)
+          return static_len(idx - 1, 0) + (name_only ? 0 : static_len(idx - 1, 1));
+        return rm;
+      };
       for (const Op &op : bl[i].ops) {
         if (op.kind == Op::SIZE) continue;
         ++nv_bound;
-        if (op.kind == Op::INDEXED) ar_bound = sat(ar_bound, rm + 2u);
-        else ar_bound = sat(ar_bound, sat(sat(op.new_name ? lit_len(op.name) : rm, lit_len(op.val)), 2u));
+        if (op.kind == Op::INDEXED) ar_bound = sat(ar_bound, ref_len(op.value, false) + 2u);
+        else
+          ar_bound = sat(ar_bound, sat(sat(op.new_name ? lit_len(op.name) : ref_len(op.value, true),
+                                           lit_len(op.val)), 2u));
       }
       may_cut = nv_bound > nva_cap || ar_bound > arena_cap;
     }
@@ -677,6 +686,8 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     snap.reserve(conns.size());
     for (auto *c : conns) snap.push_back(*c);
   }
+  if (nh && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NGHTTP2_AMD_ERR_FATAL;
+  ph.mark("host overlap + gpu wait");
   // per-block field buffers, kept across calls (under the engine's lock):
   // replay allocates only while they grow
   std::vector<BlockOut> &outs = E.outs;
