@@ -634,3 +634,18 @@ def test_fresh_codec_on_a_side_stream(dev):
     do = do.cpu().numpy().view(np.uint32).astype(np.int64)
     rel = np.arange(int(raw.sum())) - np.repeat(np.cumsum(raw) - raw, raw)
     assert np.array_equal(d[np.repeat(do[:-1], raw) + rel], pool[:int(off[-1])])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pick", ["pieces40", "items64"])
+@pytest.mark.parametrize("n", [1, 31, 33, 63, 65, 1000, 2049, 5000, 70001])
+def test_decode_instance_batch_sizes(codec, dev, n, pick):
+    """Each decode instance's task claiming at every batch size shape: one
+    string, less than a unit, ragged units and tasks, fewer tasks than
+    waves, and ranges whose units are all tail units (claimed largest first
+    once wave 0 has ranked them) -- status, state and bytes per string
+    against the oracle."""
+    from nghttp2_amd import workloads as W
+    pool, off = W.gen_mixed_values(n, seed=1000 + n)
+    enc, eoff = O.encode_batch(pool, off, nthreads=8)
+    auto_decode_check(codec, dev, enc, eoff, "%s n=%d" % (pick, n), pick=pick, nthreads=8)
