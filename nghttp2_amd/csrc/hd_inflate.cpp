@@ -23,7 +23,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <unordered_map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -143,6 +142,8 @@ struct nghttp2_amd_hd_inflater {
   size_t min_max = UINT32_MAX;                  // min_hd_table_bufsize_max
   bool expect_size = false;                     // NGHTTP2_HD_STATE_EXPECT_TABLE_SIZE
   bool bad = false;                             // ctx.bad
+  uint64_t batch_gen = 0;                       // the inflate_blocks call that last grouped it
+  uint32_t batch_conn = 0;                      // its connection number in that call
 
   void evict_oldest() {
     bufsize -= table.bytes(table.ents[table.e_first]) + kEntryOverhead;
@@ -209,6 +210,9 @@ struct Op {
 struct Block {
   std::vector<Op> ops;
   bool parse_ok = true;
+  // the output bound's parts (pass 1): fields, bytes other than dynamic-table
+  // references, and the number of those references
+  uint64_t nv = 0, ar = 0, ndyn = 0;
 };
 
 // One block's emitted fields: name\0value\0 runs in `bytes`.
@@ -239,6 +243,9 @@ struct Engine {
   std::vector<uint64_t> hbytes;
   std::vector<const Lit *> huff;
   std::vector<uint32_t> hoff;
+  uint64_t gen = 0;  // inflate_blocks calls (the connections' grouping stamp)
+  std::vector<nghttp2_amd_hd_inflater *> conns;
+  std::vector<uint32_t> cstart, corder;  // blocks per connection, in batch order
 };
 Engine &engine() {
   static Engine e;
@@ -546,6 +553,35 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       }
     nhuff[i + 1] = c;
     E.hbytes[i + 1] = by;
+    // the block's output bound (below): a field per representation, its name
+    // and value NUL-terminated; a literal's bytes (a Huffman one at its
+    // decode bound); a static-table reference at its entry's own length, a
+    // dynamic one counted (the connection's table limit bounds it)
+    uint64_t nv = 0, ar = 0, nd = 0;
+    auto lit_len = [](const Lit &l) -> uint64_t {
+      return l.huff < 0 ? (uint64_t)l.len : (uint64_t)l.len * 8u / 5u + 1u;
+    };
+    auto ref = [&](uint32_t idx, bool name_only) {
+      if (idx >= 1 && idx <= kStaticLen)
+        ar += static_len(idx - 1, 0) + (name_only ? 0 : static_len(idx - 1, 1));
+      else
+        ++nd;
+    };
+    for (const Op &op : bl[i].ops) {
+      if (op.kind == Op::SIZE) continue;
+      ++nv;
+      ar += 2u;
+      if (op.kind == Op::INDEXED) {
+        ref(op.value, false);
+      } else {
+        if (op.new_name) ar += lit_len(op.name);
+        else ref(op.value, true);
+        ar += lit_len(op.val);
+      }
+    }
+    bl[i].nv = nv;
+    bl[i].ar = ar;
+    bl[i].ndyn = nd;
   });
   for (uint32_t i = 0; i < nblocks; ++i) {
     nhuff[i + 1] += nhuff[i];
@@ -630,70 +666,66 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   // ---- pass 2: each connection's blocks in batch order against its table
   // (one task per connection), fields into per-block buffers
   const LitSrc ls{dec, slot, hst};
-  // the batch's blocks per connection, in batch order; the parallel region
-  // only reads `lists` (a vector indexed by connection number)
-  std::unordered_map<nghttp2_amd_hd_inflater *, uint32_t> conn_of;
-  std::vector<nghttp2_amd_hd_inflater *> conns;
-  std::vector<std::vector<uint32_t>> lists;
+  // the batch's blocks per connection, in batch order (a connection is
+  // numbered at its first block by a stamp in the inflater, no hash lookups);
+  // the parallel region only reads the lists
+  std::vector<nghttp2_amd_hd_inflater *> &conns = E.conns;
+  conns.clear();
+  const uint64_t gen = ++E.gen;
   for (uint32_t i = 0; i < nblocks; ++i) {
-    auto it = conn_of.emplace(inflaters[i], (uint32_t)conns.size()).first;
-    if (it->second == conns.size()) {
-      conns.push_back(inflaters[i]);
-      lists.emplace_back();
+    nghttp2_amd_hd_inflater *c = inflaters[i];
+    if (c->batch_gen != gen) {
+      c->batch_gen = gen;
+      c->batch_conn = (uint32_t)conns.size();
+      conns.push_back(c);
     }
-    lists[it->second].push_back(i);
   }
+  std::vector<uint32_t> &cstart = E.cstart, &corder = E.corder;
+  cstart.assign(conns.size() + 1, 0);
+  corder.resize(nblocks);
+  for (uint32_t i = 0; i < nblocks; ++i) ++cstart[inflaters[i]->batch_conn + 1];
+  for (size_t c = 0; c < conns.size(); ++c) cstart[c + 1] += cstart[c];
+  {
+    std::vector<uint32_t> fill(cstart.begin(), cstart.end() - 1);
+    for (uint32_t i = 0; i < nblocks; ++i) corder[fill[inflaters[i]->batch_conn]++] = i;
+  }
+  ph.mark("group");
   // A batch that outgrows the caller's buffers is cut at the first block
   // that does not fit, and the tables replayed up to there, from snapshots.
   // The snapshots (a copy of every table) are taken only when an upper bound
-  // of the output can pass the caps: a field per representation, its name
-  // and value NUL-terminated; a literal's bytes (decoded length for a
-  // Huffman one); a table reference at most the larger of the longest static
-  // entry and the connection's table limit.
+  // of the output (pass 1's per-block parts, a dynamic-table reference at the
+  // larger of the longest static entry and the connection's table limit) can
+  // pass the caps.
   bool may_cut = false;
   {
-    std::vector<size_t> ref_max(conns.size());
-    for (size_t c = 0; c < conns.size(); ++c)
-      ref_max[c] = std::max<size_t>({64u, conns[c]->settings_max, conns[c]->bufsize_max});
     // (saturating: a table limit near SIZE_MAX must not wrap the bound)
     auto sat = [](uint64_t a, uint64_t b) -> uint64_t { return a > UINT64_MAX - b ? UINT64_MAX : a + b; };
     uint64_t nv_bound = 0, ar_bound = 0;
-    // (a Huffman literal at its decode bound: the decode is still running)
-    auto lit_len = [&](const Lit &l) -> uint64_t {
-      return l.huff < 0 ? (uint64_t)l.len : (uint64_t)l.len * 8u / 5u + 1u;
-    };
     for (uint32_t i = 0; i < nblocks && !may_cut; ++i) {
-      const uint64_t rm = std::min<uint64_t>(ref_max[conn_of[inflaters[i]]], UINT32_MAX);
-      // (a static-table reference at its entry's own length)
-      auto ref_len = [&](uint32_t idx, bool name_only) -> uint64_t {
-        if (idx >= 1 && idx <= kStaticLen)
-          return static_len(idx - 1, 0) + (name_only ? 0 : static_len(idx - 1, 1));
-        return rm;
-      };
-      for (const Op &op : bl[i].ops) {
-        if (op.kind == Op::SIZE) continue;
-        ++nv_bound;
-        if (op.kind == Op::INDEXED) ar_bound = sat(ar_bound, ref_len(op.value, false) + 2u);
-        else
-          ar_bound = sat(ar_bound, sat(sat(op.new_name ? lit_len(op.name) : ref_len(op.value, true),
-                                           lit_len(op.val)), 2u));
-      }
+      const nghttp2_amd_hd_inflater *c = inflaters[i];
+      const uint64_t rm = std::min<uint64_t>(
+          std::max<size_t>({64u, c->settings_max, c->bufsize_max}), UINT32_MAX);
+      const Block &b = bl[i];
+      const uint64_t dyn = b.ndyn && rm > UINT64_MAX / b.ndyn ? UINT64_MAX : b.ndyn * rm;
+      nv_bound += b.nv;
+      ar_bound = sat(ar_bound, sat(b.ar, dyn));
       may_cut = nv_bound > nva_cap || ar_bound > arena_cap;
     }
   }
+  ph.mark("bound");
   std::vector<nghttp2_amd_hd_inflater> snap;
   if (may_cut) {
     snap.reserve(conns.size());
     for (auto *c : conns) snap.push_back(*c);
   }
   if (nh && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NGHTTP2_AMD_ERR_FATAL;
-  ph.mark("host overlap + gpu wait");
+  ph.mark("gpu wait");
   // per-block field buffers, kept across calls (under the engine's lock):
   // replay allocates only while they grow
   std::vector<BlockOut> &outs = E.outs;
   if (outs.size() < nblocks) outs.resize(nblocks);
   parallel_for(conns.size(), 1, [&](size_t c) {
-    for (uint32_t i : lists[c]) replay_block(conns[c], bl[i], ls, outs[i]);
+    for (uint32_t j = cstart[c]; j < cstart[c + 1]; ++j) replay_block(conns[c], bl[corder[j]], ls, outs[corder[j]]);
   });
 
   ph.mark("replay");
