@@ -214,7 +214,7 @@ def main():
         all_off = np.zeros(n_total + 1, dtype=np.int64)
         np.cumsum(lengths, out=all_off[1:])
         s0, s1 = S.byte_balanced_bounds(all_off, world)[rank_]
-        pool, off = W.gen_mixed_range(lengths, s0, s1)
+        pool, off = W.gen_mixed_range(lengths, s0, s1, threads=max(1, min(8, 16 // world)))
         return pool, off, "strong", "numpy PCG64, chunk-seeded 0x%X, shard [%d, %d) of %d" % (
             W.SEED[4], s0, s1, n_total)
 
@@ -333,7 +333,9 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
         rk = int(os.environ.get("RANK", "0"))
         np.savez(os.path.join(args.dump_dir, "rank%d.npz" % rk), data=np.array(data),
                  enc=P0.enc[:enc_total].cpu().numpy(),
-                 enc_off=P0.enc_off.cpu().numpy().view(np.uint32), status=st)
+                 enc_off=P0.enc_off.cpu().numpy().view(np.uint32), status=st,
+                 dec=P0.dec[:int(P0.dec_off[-1].item()) & 0xFFFFFFFF].cpu().numpy(),
+                 dec_off=P0.dec_off.cpu().numpy().view(np.uint32))
 
     progress("config %d: round trip checked, timing" % cfg)
     # per-kernel timing (roofline): K plain steps with events on the stream

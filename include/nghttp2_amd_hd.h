@@ -46,6 +46,7 @@ extern "C" {
 #define NGHTTP2_AMD_ERR_INVALID_ARGUMENT (-501) /* nghttp2.h:278 */
 #define NGHTTP2_AMD_ERR_BUFFER_ERROR (-502)     /* nghttp2.h:282 */
 #define NGHTTP2_AMD_ERR_HEADER_COMP (-523)      /* nghttp2.h:378 */
+#define NGHTTP2_AMD_ERR_INSUFF_BUFSIZE (-525)   /* nghttp2.h:386 */
 #define NGHTTP2_AMD_ERR_FATAL (-900)            /* nghttp2.h:451 (HIP error) */
 #define NGHTTP2_AMD_ERR_NOMEM (-901)            /* nghttp2.h:455 */
 
@@ -122,10 +123,14 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_huff_encode_workspace_size(uint64_t raw
  * dst_cap is, and no offset of the batch is valid.  A batch holding a
  * string longer than NGHTTP2_AMD_ENCODE_MAX_STRING raw bytes (its code bits
  * would not fit the kernels' 32-bit counts), or a tile of 256 consecutive
- * strings (256 k .. 256 k + 255) whose encoded output reaches
+ * strings (256 k .. 256 k + 255) whose encoded output may reach
  * NGHTTP2_AMD_ENCODE_MAX_TILE bytes (a wave places its output bits in 32-bit
- * positions), is marked the same way.  Header strings are far below both
- * (nghttp2 caps a field at 64 KiB, NGHTTP2_HD_MAX_NV).
+ * positions), is marked the same way.  The tile test is conservative: it
+ * sums each string's output rounded down to 64 KiB units and marks the tile
+ * when that sum comes within 256 units of 2^13 (2^29 bytes), so a tile whose
+ * output is between 2^29 - 16 MiB and 2^29 bytes may be marked too.  Header
+ * strings are far below both (nghttp2 caps a field at 64 KiB,
+ * NGHTTP2_HD_MAX_NV).
  */
 #define NGHTTP2_AMD_ENCODE_MAX_STRING (0xFFFFFFFFu / 30u)
 #define NGHTTP2_AMD_ENCODE_MAX_TILE (1u << 29)
@@ -344,7 +349,11 @@ NGHTTP2_AMD_EXTERN size_t nghttp2_amd_hd_inflate_get_max_dynamic_table_size(nght
  * a time; the inflater turns bad), or NGHTTP2_AMD_ERR_BUFFER_ERROR when
  * nva / arena ran out (that block and the rest are not applied).  The GPU
  * work is asynchronous on `stream` and synchronised before return; a batch
- * without Huffman literals makes no GPU call.
+ * without Huffman literals makes no GPU call.  The library keeps one
+ * process-wide engine (pinned and device buffers, parse state) for this
+ * call, so concurrent calls are serialised whole, host passes included; the
+ * engine keeps its per-block buffers across calls and releases the surplus
+ * when a call is far smaller than an earlier one.
  */
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters,
                                   uint32_t nblocks, const uint8_t *const *blocks,
@@ -416,6 +425,53 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *co
                                   uint32_t nblocks, const nghttp2_amd_nv *nva,
                                   const uint32_t *block_nv_off, uint8_t *out, size_t out_cap,
                                   uint32_t *out_off, int32_t *block_status, void *stream);
+
+/*
+ * One header list into a caller buffer, as nghttp2_hd_deflate_hd2
+ * (nghttp2.h:6127; lib/nghttp2_hd.c:1525-1555): the wire length, or
+ * NGHTTP2_AMD_ERR_INSUFF_BUFSIZE when buflen is too small (the deflater
+ * turns bad, as the reference's does), or NGHTTP2_AMD_ERR_HEADER_COMP for a
+ * deflater already bad.  A batch of one list on nghttp2_amd_hd_deflate_blocks
+ * (its literals framed by the GPU); host buffers, synchronous.
+ */
+NGHTTP2_AMD_EXTERN ptrdiff_t nghttp2_amd_hd_deflate_hd2(nghttp2_amd_hd_deflater *deflater,
+                                                         uint8_t *buf, size_t buflen,
+                                                         const nghttp2_amd_nv *nva, size_t nvlen,
+                                                         void *stream);
+
+/* Same layout as nghttp2_vec (nghttp2.h:5910-5919). */
+typedef struct {
+  uint8_t *base;
+  size_t len;
+} nghttp2_amd_vec;
+
+/*
+ * nghttp2_hd_deflate_hd_vec2 (nghttp2.h:6179; lib/nghttp2_hd.c:1563-1594):
+ * as nghttp2_amd_hd_deflate_hd2, the wire written across the chunks
+ * vec[0..veclen) in order (each filled before the next); INSUFF_BUFSIZE when
+ * their total is too small, including veclen == 0 and zero-length chunks.
+ */
+NGHTTP2_AMD_EXTERN ptrdiff_t nghttp2_amd_hd_deflate_hd_vec2(nghttp2_amd_hd_deflater *deflater,
+                                                             const nghttp2_amd_vec *vec,
+                                                             size_t veclen,
+                                                             const nghttp2_amd_nv *nva,
+                                                             size_t nvlen, void *stream);
+
+/*
+ * The HPACK prefix-integer decoder the inflate front-end parses with, as
+ * nghttp2_hd_decode_length (lib/nghttp2_hd.h:416-419; lib/nghttp2_hd.c:
+ * 882-945), resumable byte by byte: decode from in[0..last - in) with a
+ * `prefix`-bit first byte, continuing a previous call's partial value
+ * `initial` at `shift` (both 0 at the start of an integer).  Returns the
+ * bytes consumed, or -1 on overflow past UINT32_MAX (a shift of 32 bits or
+ * more included); *fin = 1 once the integer is complete (*res its value),
+ * else *res and *shift_ptr carry the partial state to the next call.
+ * Host-only.
+ */
+NGHTTP2_AMD_EXTERN ptrdiff_t nghttp2_amd_hd_decode_length(uint32_t *res, size_t *shift_ptr, int *fin,
+                                                           uint32_t initial, size_t shift,
+                                                           const uint8_t *in, const uint8_t *last,
+                                                           size_t prefix);
 
 /* ------------------------------------------------------------------ */
 /* One batch over several GPUs                       */

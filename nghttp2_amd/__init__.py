@@ -13,7 +13,9 @@ from .hd import (  # noqa: F401
     HuffmanBatchCodec,
     NGHTTP2_ERR_BUFFER_ERROR,
     NGHTTP2_ERR_HEADER_COMP,
+    NGHTTP2_ERR_INSUFF_BUFSIZE,
     NGHTTP2_ERR_INVALID_ARGUMENT,
+    decode_length,
     lib,
     lib_path,
     deflate_blocks,

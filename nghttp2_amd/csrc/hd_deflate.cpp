@@ -575,4 +575,43 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
   return ret;
 }
 
+ptrdiff_t nghttp2_amd_hd_deflate_hd2(nghttp2_amd_hd_deflater *deflater, uint8_t *buf, size_t buflen,
+                                     const nghttp2_amd_nv *nva, size_t nvlen, void *stream) {
+  if (!deflater || (!buf && buflen) || (!nva && nvlen) || nvlen > UINT32_MAX)
+    return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  const uint32_t nv_off[2] = {0, (uint32_t)nvlen};
+  uint32_t out_off[2] = {0, 0};
+  int32_t st = 0;
+  uint8_t none = 0;
+  const int rv = nghttp2_amd_hd_deflate_blocks(&deflater, 1, nva, nv_off, buf ? buf : &none, buflen,
+                                               out_off, &st, stream);
+  if (st == NGHTTP2_AMD_ERR_BUFFER_ERROR) return NGHTTP2_AMD_ERR_INSUFF_BUFSIZE;  // :1546-1547
+  if (st < 0) return st;
+  if (rv < 0) return rv;
+  return (ptrdiff_t)st;
+}
+
+ptrdiff_t nghttp2_amd_hd_deflate_hd_vec2(nghttp2_amd_hd_deflater *deflater, const nghttp2_amd_vec *vec,
+                                         size_t veclen, const nghttp2_amd_nv *nva, size_t nvlen,
+                                         void *stream) {
+  if (!deflater || (!vec && veclen)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  size_t total = 0;
+  for (size_t i = 0; i < veclen; ++i) {
+    if (!vec[i].base && vec[i].len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+    total += vec[i].len;
+  }
+  // the wire into one contiguous buffer of the chunks' total, then across
+  // the chunks in order (nghttp2_bufs_wrap_init2 fills them one by one)
+  std::vector<uint8_t> tmp(total);
+  const ptrdiff_t n = nghttp2_amd_hd_deflate_hd2(deflater, tmp.data(), total, nva, nvlen, stream);
+  if (n < 0) return n;
+  size_t o = 0;
+  for (size_t i = 0; i < veclen && o < (size_t)n; ++i) {
+    const size_t k = std::min(vec[i].len, (size_t)n - o);
+    memcpy(vec[i].base, tmp.data() + o, k);
+    o += k;
+  }
+  return n;
+}
+
 }  // extern "C"

@@ -69,12 +69,17 @@ struct Engine {
   bool kept = false;
   std::vector<uint8_t> kept_src, kept_out;
 
-  ~Engine() {
-    if (!ready) return;
+  ~Engine() { release(); }
+  void release() {
     if (d_buf) (void)hipFree(d_buf);
     if (h_pin) (void)hipHostFree(h_pin);
     if (d_ws) (void)hipFree(d_ws);
     if (st) (void)hipStreamDestroy(st);
+    d_buf = h_pin = nullptr;
+    d_ws = nullptr;
+    st = nullptr;
+    cap = ws = 0;
+    ready = false;
   }
   // the thread's stream and buffers on its current device; grows to `need`
   bool reserve(size_t need) {
@@ -85,10 +90,19 @@ struct Engine {
       new (this) Engine();
     }
     if (!ready) {
+      // (a failed init releases what it made: a thread whose allocations
+      // keep failing does not leak a stream per call)
       device = dev;
-      if (!hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking))) return false;
+      if (!hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking))) {
+        st = nullptr;
+        return false;
+      }
       ws = nghttp2_amd_hd_huff_workspace_size(1);
-      if (!hip_ok(hipMalloc(&d_ws, ws))) return false;
+      if (!hip_ok(hipMalloc(&d_ws, ws))) {
+        d_ws = nullptr;
+        release();
+        return false;
+      }
       ready = true;
     }
     if (need > cap) {

@@ -169,28 +169,16 @@ struct nghttp2_amd_hd_inflater {
 namespace {
 
 // decode_length (lib/nghttp2_hd.c:882-945) for a whole block: the prefix
-// integer at in[*pos]; false on overflow or truncation.
+// integer at in[*pos] (the resumable decoder below, which must finish
+// inside the block: the block is complete, in_final); false on overflow or
+// truncation.
 bool read_int(const uint8_t *in, size_t len, size_t *pos, uint32_t prefix, uint32_t *out) {
   if (*pos >= len) return false;
-  const uint32_t k = (1u << prefix) - 1u;
-  uint32_t n = in[*pos] & k;
-  ++*pos;
-  if (n != k) {
-    *out = n;
-    return true;
-  }
-  for (uint32_t shift = 0;; shift += 7) {
-    if (*pos >= len) return false;  // truncated (in_final)
-    const uint32_t b = in[(*pos)++];
-    uint32_t add = b & 0x7Fu;
-    if (shift >= 32) return false;
-    if ((UINT32_MAX >> shift) < add) return false;
-    add <<= shift;
-    if (UINT32_MAX - add < n) return false;
-    n += add;
-    if (!(b & 0x80u)) break;
-  }
-  *out = n;
+  size_t shift = 0;
+  int fin = 0;
+  const ptrdiff_t n = nghttp2_amd_hd_decode_length(out, &shift, &fin, 0, 0, in + *pos, in + len, prefix);
+  if (n < 0 || !fin) return false;
+  *pos += (size_t)n;
   return true;
 }
 
@@ -462,6 +450,53 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
 
 extern "C" {
 
+// The prefix integer (RFC 7541 5.1) as nghttp2_hd_decode_length
+// (lib/nghttp2_hd.c:882-945): the first byte's low `prefix` bits, then
+// 7-bit groups least significant first while the top bit is set; the value
+// must stay within uint32 (a group at a shift of 32 or more, or one that
+// carries past UINT32_MAX, is -1).  `initial`/`shift` continue a partial
+// integer from an earlier call (initial == 0: a fresh one).
+ptrdiff_t nghttp2_amd_hd_decode_length(uint32_t *res, size_t *shift_ptr, int *fin, uint32_t initial,
+                                       size_t shift, const uint8_t *in, const uint8_t *last,
+                                       size_t prefix) {
+  const uint8_t *p = in;
+  uint32_t v = initial;
+  *shift_ptr = 0;
+  *fin = 0;
+  if (p == last) {  // (nothing to read: the state stays as it was)
+    *res = v;
+    *shift_ptr = shift;
+    return 0;
+  }
+  if (v == 0) {  // the prefix byte
+    const uint32_t mask = (1u << prefix) - 1u;
+    const uint32_t low = *p++ & mask;
+    if (low < mask) {
+      *res = low;
+      *fin = 1;
+      return 1;
+    }
+    v = mask;
+  }
+  for (; p != last; shift += 7) {
+    const uint8_t b = *p++;
+    const uint32_t grp = b & 0x7Fu;
+    if (shift >= 32 || grp > (UINT32_MAX >> shift)) return -1;
+    const uint32_t add = grp << shift;
+    if (add > UINT32_MAX - v) return -1;
+    v += add;
+    if (!(b & 0x80u)) {
+      *res = v;
+      *shift_ptr = shift;
+      *fin = 1;
+      return p - in;
+    }
+  }
+  *res = v;
+  *shift_ptr = shift;
+  return p - in;
+}
+
 int nghttp2_amd_hd_inflate_new(nghttp2_amd_hd_inflater **inflater_ptr) {
   if (!inflater_ptr) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   *inflater_ptr = new (std::nothrow) nghttp2_amd_hd_inflater();
@@ -535,6 +570,18 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   nghttp2_amd_host::Phases ph("inflate");
   std::lock_guard<std::mutex> guard(engine().mu);
   Engine &E = engine();
+  // the per-block buffers are kept across calls so a warm call allocates
+  // nothing; a call far below an earlier large batch releases the surplus
+  // (a high-water mark of 2x + 4096 blocks), so one large batch does not pin
+  // its parse and output footprint for the life of the process
+  auto trim = [nblocks](auto &v) {
+    if (v.size() > 2u * (size_t)nblocks + 4096u) {
+      v.resize(nblocks);
+      v.shrink_to_fit();
+    }
+  };
+  trim(E.bl);
+  trim(E.outs);
   if (E.bl.size() < nblocks) E.bl.resize(nblocks);
   E.nhuff.assign(nblocks + 1, 0);  // Huffman literals per block, then prefix
   E.hbytes.assign(nblocks + 1, 0);  // their bytes per block, then prefix
@@ -639,14 +686,21 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     parallel_for(nh, 4096, [&](size_t k) { memcpy(E.h_pool + hoff[k], huff[k]->p, huff[k]->len); });
     memset(E.h_pool + hoff[nh], 0, in_bytes - hoff[nh]);
     memcpy(E.h_meta, hoff.data(), (nh + 1) * sizeof(uint32_t));
+    // a failure after the first copy is queued drains the stream before
+    // returning: a copy still in flight must not land in the pinned pool
+    // after the next call has filled it
+    auto drain = [st](int rv) {
+      (void)hipStreamSynchronize(st);
+      return rv;
+    };
     if (hipMemcpyAsync(E.d_in, E.h_pool, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(E.d_off, E.h_meta, (nh + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
                        st) != hipSuccess)
-      return NGHTTP2_AMD_ERR_FATAL;
+      return drain(NGHTTP2_AMD_ERR_FATAL);
     int rv = nghttp2_amd_hd_huff_decode_batch_auto(E.d_in, E.d_off, nh, (uint64_t)hoff[nh], E.d_out,
                                                    out_bytes, E.d_slot, E.d_st, nullptr, nullptr,
                                                    stream);
-    if (rv) return rv;
+    if (rv) return drain(rv);
     uint32_t *h_slot = E.h_meta + (nh + 1);
     int32_t *h_st = (int32_t *)(h_slot + (nh + 1));
     if (hipMemcpyAsync(E.h_pool, E.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -654,7 +708,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
                        st) != hipSuccess ||
         hipMemcpyAsync(h_st, E.d_st, nh * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
             hipSuccess)
-      return NGHTTP2_AMD_ERR_FATAL;
+      return drain(NGHTTP2_AMD_ERR_FATAL);
     dec = E.h_pool;
     slot = h_slot;
     hst = h_st;

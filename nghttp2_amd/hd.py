@@ -30,6 +30,7 @@ LIB_NAME = "libnghttp2_amd_hd.so"
 NGHTTP2_ERR_INVALID_ARGUMENT = -501
 NGHTTP2_ERR_BUFFER_ERROR = -502
 NGHTTP2_ERR_HEADER_COMP = -523
+NGHTTP2_ERR_INSUFF_BUFSIZE = -525
 NGHTTP2_ERR_FATAL = -900
 
 _lib = None
@@ -408,6 +409,15 @@ class HpackInflater:
     def dynamic_table_size(self):
         return self.L.nghttp2_amd_hd_inflate_get_dynamic_table_size(self.p)
 
+    def max_dynamic_table_size(self):
+        """nghttp2_hd_inflate_get_max_dynamic_table_size: the table limit in
+        force (the reference's ctx.hd_table_bufsize_max)."""
+        return self.L.nghttp2_amd_hd_inflate_get_max_dynamic_table_size(self.p)
+
+    def num_table_entries(self):
+        """nghttp2_hd_inflate_get_num_table_entries: static (61) + dynamic."""
+        return self.L.nghttp2_amd_hd_inflate_get_num_table_entries(self.p)
+
 
 _NV_DTYPE = np.dtype([("block", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
                       ("value_off", "<u4"), ("value_len", "<u4"), ("flags", "u1")], align=True)
@@ -514,6 +524,18 @@ def _deflate_lib():
         L.nghttp2_amd_hd_deflate_get_dynamic_table_size.argtypes = [vp]
         L.nghttp2_amd_hd_deflate_get_dynamic_table_size.restype = sz
         L.nghttp2_amd_hd_deflate_blocks.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, sz, vp, vp, vp]
+        L.nghttp2_amd_hd_deflate_get_max_dynamic_table_size.argtypes = [vp]
+        L.nghttp2_amd_hd_deflate_get_max_dynamic_table_size.restype = sz
+        L.nghttp2_amd_hd_deflate_bound.argtypes = [vp, vp, sz]
+        L.nghttp2_amd_hd_deflate_bound.restype = sz
+        L.nghttp2_amd_hd_deflate_hd2.argtypes = [vp, vp, sz, vp, sz, vp]
+        L.nghttp2_amd_hd_deflate_hd2.restype = ctypes.c_ssize_t
+        L.nghttp2_amd_hd_deflate_hd_vec2.argtypes = [vp, vp, sz, vp, sz, vp]
+        L.nghttp2_amd_hd_deflate_hd_vec2.restype = ctypes.c_ssize_t
+        L.nghttp2_amd_hd_decode_length.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(sz),
+                                                   ctypes.POINTER(ctypes.c_int), ctypes.c_uint32, sz,
+                                                   vp, vp, sz]
+        L.nghttp2_amd_hd_decode_length.restype = ctypes.c_ssize_t
         L._deflate_bound = True
     return L
 
@@ -553,11 +575,88 @@ class HpackDeflater:
     def dynamic_table_size(self):
         return self.L.nghttp2_amd_hd_deflate_get_dynamic_table_size(self.p)
 
+    def max_dynamic_table_size(self):
+        """nghttp2_hd_deflate_get_max_dynamic_table_size (the reference's
+        ctx.hd_table_bufsize_max)."""
+        return self.L.nghttp2_amd_hd_deflate_get_max_dynamic_table_size(self.p)
 
-def deflate_blocks(deflaters, header_lists, stream=None):
+    def num_table_entries(self):
+        return self.L.nghttp2_amd_hd_deflate_get_num_table_entries(self.p)
+
+    def bound(self, header_list):
+        """nghttp2_hd_deflate_bound of one list."""
+        nva, keep = _nv_array(header_list)
+        return self.L.nghttp2_amd_hd_deflate_bound(self.p, nva.ctypes.data, len(header_list))
+
+    def deflate_hd2(self, header_list, buflen, stream=None):
+        """nghttp2_hd_deflate_hd2 into a buffer of buflen bytes: (rv, wire);
+        rv is the length or NGHTTP2_ERR_INSUFF_BUFSIZE / HEADER_COMP."""
+        nva, keep = _nv_array(header_list)
+        buf = np.zeros(max(1, buflen), dtype=np.uint8)
+        rv = self.L.nghttp2_amd_hd_deflate_hd2(self.p, buf.ctypes.data, buflen, nva.ctypes.data,
+                                               len(header_list), _cur_stream(stream))
+        return rv, (buf[:rv].tobytes() if rv >= 0 else b"")
+
+    def deflate_hd_vec2(self, header_list, chunk_lens, stream=None):
+        """nghttp2_hd_deflate_hd_vec2 over chunks of the given lengths (None:
+        a NULL vector of length 0): (rv, [chunk bytes])."""
+        nva, keep = _nv_array(header_list)
+        if chunk_lens is None:
+            rv = self.L.nghttp2_amd_hd_deflate_hd_vec2(self.p, None, 0, nva.ctypes.data,
+                                                       len(header_list), _cur_stream(stream))
+            return rv, []
+        bufs = [np.zeros(max(1, n), dtype=np.uint8) for n in chunk_lens]
+        vec = (_Vec * max(1, len(chunk_lens)))()
+        for k, (b, n) in enumerate(zip(bufs, chunk_lens)):
+            vec[k].base = b.ctypes.data if n else None
+            vec[k].len = n
+        rv = self.L.nghttp2_amd_hd_deflate_hd_vec2(self.p, vec, len(chunk_lens), nva.ctypes.data,
+                                                   len(header_list), _cur_stream(stream))
+        return rv, [b[:n].tobytes() for b, n in zip(bufs, chunk_lens)]
+
+
+class _Vec(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+def _cur_stream(stream):
+    if stream is not None:
+        return ctypes.c_void_p(stream.cuda_stream)
+    import torch
+    if torch.cuda.is_available():
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return None
+
+
+def _nv_array(header_list):
+    """An nghttp2_nv-layout array over one list's (name, value[, flags]);
+    returns (array, buffers kept alive)."""
+    nva = np.zeros(max(1, len(header_list)), dtype=_NVIN_DTYPE)
+    keep = []
+    for k, h in enumerate(header_list):
+        n, v = np.frombuffer(bytes(h[0]) + b"\0", np.uint8), np.frombuffer(bytes(h[1]) + b"\0", np.uint8)
+        keep += [n, v]
+        nva[k] = (n.ctypes.data, v.ctypes.data, len(h[0]), len(h[1]), h[2] if len(h) > 2 else 0)
+    return nva, keep
+
+
+def decode_length(data, prefix, initial=0, shift=0):
+    """nghttp2_hd_decode_length over bytes `data`: (rv, value, shift, fin)."""
+    L = _deflate_lib()
+    buf = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8)
+    res, sh, fin = ctypes.c_uint32(), ctypes.c_size_t(), ctypes.c_int()
+    base = buf.ctypes.data
+    rv = L.nghttp2_amd_hd_decode_length(ctypes.byref(res), ctypes.byref(sh), ctypes.byref(fin),
+                                        initial, shift, base, base + len(data), prefix)
+    return rv, res.value, sh.value, fin.value
+
+
+def deflate_blocks(deflaters, header_lists, stream=None, out_cap=None):
     """Encode header lists (each [(name, value[, flags])]), list i with
     deflaters[i]; every literal framed in one GPU batch.  Returns
-    (status[i], wire[i])."""
+    (status[i], wire[i]).  out_cap (default: room for every list) limits the
+    output: a list that does not fit gets NGHTTP2_ERR_BUFFER_ERROR and its
+    deflater turns bad."""
     L = _deflate_lib()
     nb = len(header_lists)
     flat = [(bytes(h[0]), bytes(h[1]), (h[2] if len(h) > 2 else 0))
@@ -584,8 +683,8 @@ def deflate_blocks(deflaters, header_lists, stream=None):
     if nb:
         np.cumsum(np.fromiter((len(hl) for hl in header_lists), dtype=np.uint32, count=nb),
                   out=offs[1:])
-    cap = int(plen.sum()) + 16 * nf + 16 * nb + 64
-    out = np.empty(cap, dtype=np.uint8)
+    cap = int(plen.sum()) + 16 * nf + 16 * nb + 64 if out_cap is None else out_cap
+    out = np.empty(max(1, cap), dtype=np.uint8)
     out_off = np.zeros(nb + 1, dtype=np.uint32)
     st = np.zeros(max(1, nb), dtype=np.int32)
     defl = np.fromiter((d.p.value for d in deflaters), dtype=np.uint64, count=nb) if nb \

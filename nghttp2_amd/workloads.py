@@ -84,20 +84,30 @@ def mixed_lengths(n, seed=SEED[4], lo=16, hi=1024):
     return out
 
 
-def gen_mixed_range(lengths, s0, s1, seed=SEED[4]):
+def _mixed_chunk(lengths, c, s0, s1, seed):
+    c0, c1 = c * CHUNK, min((c + 1) * CHUNK, len(lengths))
+    rng = np.random.Generator(np.random.PCG64([seed, 1 << 20, c]))
+    tot = int(lengths[c0:c1].sum())
+    cookie = rng.choice(COOKIE_ALPHABET, size=tot)
+    other = rng.choice(PRINTABLE, size=tot)
+    chars = np.where(rng.random(tot) < 0.85, cookie, other).astype(np.uint8)
+    cum = np.concatenate([[0], np.cumsum(lengths[c0:c1])])
+    a, b = max(s0, c0) - c0, min(s1, c1) - c0
+    return chars[cum[a]:cum[b]]
+
+
+def gen_mixed_range(lengths, s0, s1, seed=SEED[4], threads=1):
     """Characters of strings [s0, s1) of a chunk-seeded config-4 set: each
-    rank generates only its own shard.  Returns (pool, off) rebased to 0."""
-    parts = []
-    for c in range(s0 // CHUNK, (max(s1, s0 + 1) - 1) // CHUNK + 1):
-        c0, c1 = c * CHUNK, min((c + 1) * CHUNK, len(lengths))
-        rng = np.random.Generator(np.random.PCG64([seed, 1 << 20, c]))
-        tot = int(lengths[c0:c1].sum())
-        cookie = rng.choice(COOKIE_ALPHABET, size=tot)
-        other = rng.choice(PRINTABLE, size=tot)
-        chars = np.where(rng.random(tot) < 0.85, cookie, other).astype(np.uint8)
-        cum = np.concatenate([[0], np.cumsum(lengths[c0:c1])])
-        a, b = max(s0, c0) - c0, min(s1, c1) - c0
-        parts.append(chars[cum[a]:cum[b]])
+    rank generates only its own shard.  Returns (pool, off) rebased to 0.
+    The chunks are seeded independently, so `threads` > 1 (a thread pool;
+    numpy releases the GIL in the generators) gives the same bytes."""
+    chunks = list(range(s0 // CHUNK, (max(s1, s0 + 1) - 1) // CHUNK + 1))
+    if threads > 1 and len(chunks) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as ex:
+            parts = list(ex.map(lambda c: _mixed_chunk(lengths, c, s0, s1, seed), chunks))
+    else:
+        parts = [_mixed_chunk(lengths, c, s0, s1, seed) for c in chunks]
     chars = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
     return _pool_from_lengths(lengths[s0:s1], chars)
 

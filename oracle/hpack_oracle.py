@@ -188,6 +188,54 @@ class Inflater:
             raise _Fail()
 
 
+def block_has_huffman(b):
+    """Whether a complete block carries a Huffman string literal (the H bit of
+    any literal): the wire is self-delimiting, so this is a stateless scan of
+    the representations (lib/nghttp2_hd.c:1919-2288's opcode and literal
+    framing).  Test infrastructure: which product cases need the GPU."""
+    b = bytes(b)
+    pos = 0
+
+    def skip_int(prefix):
+        nonlocal pos
+        k = (1 << prefix) - 1
+        n = b[pos] & k
+        pos += 1
+        if n == k:
+            shift = 0
+            while True:
+                c = b[pos]
+                pos += 1
+                n += (c & 0x7F) << shift
+                shift += 7
+                if not c & 0x80:
+                    break
+        return n
+
+    def lit():
+        nonlocal pos
+        h = b[pos] & 0x80
+        n = skip_int(7)
+        pos += n
+        return bool(h)
+
+    found = False
+    while pos < len(b):
+        c = b[pos]
+        if (c & 0xE0) == 0x20:
+            skip_int(5)
+        elif c & 0x80:
+            skip_int(7)
+        else:
+            if c in (0x40, 0x00, 0x10):
+                pos += 1
+                found |= lit()
+            else:
+                skip_int(6 if c & 0x40 else 4)
+            found |= lit()
+    return found
+
+
 # ---------------------------------------------------------------------------
 # Deflater (nghttp2_hd_deflate_hd2 per block)
 # ---------------------------------------------------------------------------

@@ -100,8 +100,13 @@ static void check_decode(const batch *e, const uint8_t *d, const uint32_t *doff,
   free(buf);
 }
 
+/* the device of each shard: device 0 repeated, or (several GPUs) distinct
+ * devices, which exercises the per-thread hipSetDevice, the per-device
+ * persistent-grid cache and per-device workspaces and streams */
+static int g_devs[4] = {0, 0, 0, 0};
+
 static void host_variant(uint32_t nshards, const batch *r, const batch *e, const batch *bad) {
-  int devs[4] = {0, 0, 0, 0};
+  int *devs = g_devs;
   nghttp2_amd_hd_sharded *s = NULL;
   CHECK(nghttp2_amd_hd_sharded_new(&s, devs, nshards) == 0, "sharded_new");
   CHECK(nghttp2_amd_hd_sharded_count(s) == nshards, "count");
@@ -144,7 +149,7 @@ static void host_variant(uint32_t nshards, const batch *r, const batch *e, const
 
 /* device-resident: the caller cuts, each shard's buffers on "its" device */
 static void dev_variant(uint32_t nshards, const batch *r, const batch *e) {
-  int devs[4] = {0, 0, 0, 0};
+  int *devs = g_devs;
   nghttp2_amd_hd_sharded *s = NULL;
   CHECK(nghttp2_amd_hd_sharded_new(&s, devs, nshards) == 0, "sharded_new");
   uint32_t cuts[5];
@@ -160,6 +165,7 @@ static void dev_variant(uint32_t nshards, const batch *r, const batch *e) {
     for (uint32_t i = 0; i <= n; ++i) o[i] = r->off[s0 + i] - a;  /* rebased */
     void *src, *soff, *dst, *doff;
     const size_t cap = nghttp2_amd_hd_huff_encode_bound(b - a, n);
+    CHECK(hipSetDevice(devs[k]) == hipSuccess, "hipSetDevice");
     CHECK(hipMalloc(&src, (b - a) + 64) == hipSuccess && hipMalloc(&soff, 4u * (n + 1)) == hipSuccess &&
               hipMalloc(&dst, cap) == hipSuccess && hipMalloc(&doff, 4u * (n + 1)) == hipSuccess, "hipMalloc");
     CHECK(hipMemcpy(src, r->pool + a, (b - a) + 32, hipMemcpyHostToDevice) == hipSuccess, "H2D");
@@ -177,6 +183,7 @@ static void dev_variant(uint32_t nshards, const batch *r, const batch *e) {
     CHECK(sh[k].out_bytes == e->off[cuts[k + 1]] - e->off[s0], "shard bytes");
     uint8_t *out = malloc(sh[k].out_bytes + 1);
     uint32_t *oo = malloc(4u * (n + 1));
+    CHECK(hipSetDevice(devs[k]) == hipSuccess, "hipSetDevice");
     CHECK(hipMemcpy(out, sh[k].dst, sh[k].out_bytes, hipMemcpyDeviceToHost) == hipSuccess, "D2H");
     CHECK(hipMemcpy(oo, sh[k].dst_off, 4u * (n + 1), hipMemcpyDeviceToHost) == hipSuccess, "D2H");
     for (uint32_t i = 0; i <= n; ++i) CHECK(oo[i] + sh[k].out_base == e->off[s0 + i], "dev offsets");
@@ -196,6 +203,7 @@ static void dev_variant(uint32_t nshards, const batch *r, const batch *e) {
     uint8_t *d = malloc(dh[k].out_bytes + 1);
     uint32_t *doff = malloc(4u * (n + 1));
     int32_t *st = malloc(4u * (n + 1));
+    CHECK(hipSetDevice(devs[k]) == hipSuccess, "hipSetDevice");
     CHECK(hipMemcpy(d, dh[k].dst, dh[k].out_bytes, hipMemcpyDeviceToHost) == hipSuccess, "D2H");
     CHECK(hipMemcpy(doff, dh[k].dst_off, 4u * (n + 1), hipMemcpyDeviceToHost) == hipSuccess, "D2H");
     CHECK(hipMemcpy(st, dh[k].status, 4u * n + 4, hipMemcpyDeviceToHost) == hipSuccess, "D2H");
@@ -209,6 +217,7 @@ static void dev_variant(uint32_t nshards, const batch *r, const batch *e) {
     (void)hipFree(dh[k].dst), (void)hipFree(dh[k].dst_off), (void)hipFree(dh[k].status);
     free(d), free(doff), free(st);
   }
+  CHECK(hipSetDevice(0) == hipSuccess, "hipSetDevice");
   nghttp2_amd_hd_sharded_del(s);
 }
 
@@ -228,6 +237,16 @@ int main(void) {
   /* more shards than strings */
   batch r3 = gen_raw(2), e3 = oracle_encode(&r3);
   host_variant(3, &r3, &e3, &e3);
+  /* several GPUs: the same checks with distinct devices per shard */
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 1) {
+    for (int k = 0; k < 4; ++k) g_devs[k] = k % ndev;
+    for (uint32_t m = 2; m <= 4; ++m) {
+      host_variant(m, &r, &e, &bad);
+      dev_variant(m, &r, &e);
+    }
+    printf("sharded OK on %d devices\n", ndev < 4 ? ndev : 4);
+  }
   printf("sharded OK\n");
   return 0;
 }

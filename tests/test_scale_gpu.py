@@ -341,38 +341,69 @@ def _free_port():
     return p
 
 
-def test_bench_two_ranks_gloo_one_gpu(dev, tmp_path):
+def _bench_ranks_gloo_one_gpu(nranks, total, tmp_path):
     """bench.py's N > 1 path (init, byte-balanced config-4 shard per rank,
-    barrier, max-over-ranks time, summed bytes) as 2 ranks on the one GPU,
-    collectives over gloo; each rank's encoded shard (bytes and offsets) is
-    then checked against the oracle's encode of the same shard, and its
-    decode status against the raw lengths."""
+    barrier, max-over-ranks time, summed bytes) as `nranks` ranks on the one
+    GPU, collectives over gloo; each rank's encoded shard (bytes and offsets)
+    is then checked against the oracle's encode of the same shard, and its
+    decode (status, dense offsets and every decoded byte) against the
+    shard's raw strings."""
     from nghttp2_amd import shard as S
     from nghttp2_amd import workloads as W
-    total = 1 << 21
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % nranks,
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--config", "4",
-           "--strings", str(total), "--steps", "3", "--warmup", "1", "--streams", "1",
-           "--no-cpu-baseline", "--dump-dir", str(tmp_path)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
-    assert r.returncode == 0, r.stderr[-3000:]
+           os.path.join(REPO, "bench.py"), "--gpus", str(nranks), "--backend", "gloo",
+           "--config", "4", "--strings", str(total), "--steps", "3", "--warmup", "1",
+           "--streams", "1", "--no-cpu-baseline", "--dump-dir", str(tmp_path)]
+    # (rank 0's progress lines pass through to the test's output: a long run
+    # keeps printing)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=540, env=env, cwd=REPO)
+    assert r.returncode == 0, "bench.py ranks failed (rc %d)" % r.returncode
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["value"] > 0
-    # the two shards cover the set: 2 * strings_per_gpu is about 2M
-    assert abs(2 * out["config"]["strings_per_gpu"] - total) < 4096
+    assert out["n_gpus"] == nranks and out["scaling"] == "strong" and out["value"] > 0
+    # the shards cover the set: nranks * strings_per_gpu is about `total`
+    assert abs(nranks * out["config"]["strings_per_gpu"] - total) < 4096 * nranks
     lengths = W.mixed_lengths(total)
     all_off = np.zeros(total + 1, dtype=np.int64)
     np.cumsum(lengths, out=all_off[1:])
-    for rk, (s0, s1) in enumerate(S.byte_balanced_bounds(all_off, 2)):
+    bounds = S.byte_balanced_bounds(all_off, nranks)
+    assert bounds[0][0] == 0 and bounds[-1][1] == total
+    for rk, (s0, s1) in enumerate(bounds):
+        print("checking rank %d: strings [%d, %d)" % (rk, s0, s1), flush=True)
         d = np.load(str(tmp_path / ("rank%d.npz" % rk)))
-        pool, off = W.gen_mixed_range(lengths, s0, s1)
-        renc, reoff = O.encode_batch(pool, off, nthreads=8)
+        pool, off = W.gen_mixed_range(lengths, s0, s1, threads=8)
+        renc, reoff = O.encode_batch(pool, off, nthreads=16)
         assert np.array_equal(d["enc_off"], reoff), "rank %d: encoded offsets" % rk
         assert np.array_equal(d["enc"], renc[:int(reoff[-1])]), "rank %d: encoded bytes" % rk
-        assert np.array_equal(d["status"], np.diff(off.astype(np.int64))), "rank %d: status" % rk
+        ln = np.diff(off.astype(np.int64))
+        assert np.array_equal(d["status"], ln), "rank %d: status" % rk
+        # decoded bytes: dense per task, string i at dec_off[i]
+        do = d["dec_off"].astype(np.int64)
+        dec = d["dec"]
+        assert int(do[-1]) == len(dec) >= int(ln.sum()), "rank %d: decoded extent" % rk
+        for a in range(0, len(ln), 1 << 19):
+            b = min(len(ln), a + (1 << 19))
+            lc = ln[a:b]
+            rel = np.arange(int(lc.sum())) - np.repeat(np.cumsum(lc) - lc, lc)
+            got = dec[np.repeat(do[a:b], lc) + rel]
+            want = pool[np.repeat(off[a:b].astype(np.int64), lc) + rel]
+            assert np.array_equal(got, want), "rank %d: decoded bytes of strings [%d, %d)" % (rk, a, b)
+
+
+def test_bench_two_ranks_gloo_one_gpu(dev, tmp_path):
+    _bench_ranks_gloo_one_gpu(2, 1 << 21, tmp_path)
+
+
+@pytest.mark.timeout(900)
+def test_bench_eight_ranks_gloo_one_gpu_config4(dev, tmp_path):
+    """The 8-way split of the whole config-4 set (16M strings, BASELINE.json
+    configs[3]) as 8 bench.py ranks sharing the one GPU: each rank's encode
+    and decode checked byte for byte.  (Still one physical GPU: the 8-GPU
+    node's scaling is measured only by the driver.)"""
+    _bench_ranks_gloo_one_gpu(8, 1 << 24, tmp_path)
 
 
 def test_compat_per_call_latency(dev):

@@ -55,3 +55,37 @@ def test_sharded_codec_more_shards_than_strings(dev):
     enc, eoff = sc.encode(pool, off)
     ref, roff = O.encode_batch(pool, off)
     assert np.array_equal(enc, ref) and np.array_equal(eoff, roff.astype(np.uint64))
+
+
+@pytest.mark.timeout(900)
+def test_sharded_8way_config4_full_16m(dev):
+    """The C ABI's sharded engine cut 8 ways (8 worker threads and streams,
+    all on device 0) over the whole config-4 set, 16,777,216 strings of the
+    config-4 generator (2.5 GB raw): merged encode equal to the oracle's
+    encode of the unsharded set, byte for byte; merged decode with status ==
+    length and every decoded byte equal to the input."""
+    from nghttp2_amd.shard import ShardedCodec
+    n = 1 << 24
+    lengths = W.mixed_lengths(n)
+    pool, off = W.gen_mixed_range(lengths, 0, n, threads=16)
+    raw = int(off[-1])
+    print("generated %d strings, %d bytes" % (n, raw), flush=True)
+    sc = ShardedCodec([dev.index or 0] * 8)
+    enc, eoff = sc.encode(pool, off)
+    print("sharded encode done", flush=True)
+    ref, roff = O.encode_batch(pool, off, nthreads=16)
+    assert np.array_equal(eoff, roff.astype(np.uint64)), "merged offsets"
+    assert np.array_equal(enc, ref[:int(roff[-1])]), "merged encoded bytes"
+    del ref
+    d, do, st = sc.decode_auto(enc, roff)
+    print("sharded decode done", flush=True)
+    assert np.array_equal(st, lengths.astype(np.int32)), "merged status"
+    assert int(do[-1]) == len(d) >= raw  # (dense per task; tasks start at their bound)
+    do = do.astype(np.int64)
+    for a in range(0, n, 1 << 20):
+        b = min(n, a + (1 << 20))
+        lc = lengths[a:b]
+        rel = np.arange(int(lc.sum())) - np.repeat(np.cumsum(lc) - lc, lc)
+        got = d[np.repeat(do[a:b], lc) + rel]
+        want = pool[np.repeat(off[a:b].astype(np.int64), lc) + rel]
+        assert np.array_equal(got, want), "decoded bytes of strings [%d, %d)" % (a, b)
