@@ -364,13 +364,14 @@ def _bench_ranks_gloo_one_gpu(nranks, total, tmp_path):
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == nranks and out["scaling"] == "strong" and out["value"] > 0
-    # the shards cover the set: nranks * strings_per_gpu is about `total`
-    assert abs(nranks * out["config"]["strings_per_gpu"] - total) < 4096 * nranks
     lengths = W.mixed_lengths(total)
     all_off = np.zeros(total + 1, dtype=np.int64)
     np.cumsum(lengths, out=all_off[1:])
     bounds = S.byte_balanced_bounds(all_off, nranks)
+    # the shards cover the set, and rank 0 ran its byte-balanced shard
     assert bounds[0][0] == 0 and bounds[-1][1] == total
+    assert all(bounds[k][1] == bounds[k + 1][0] for k in range(nranks - 1))
+    assert out["config"]["strings_per_gpu"] == bounds[0][1] - bounds[0][0]
     for rk, (s0, s1) in enumerate(bounds):
         print("checking rank %d: strings [%d, %d)" % (rk, s0, s1), flush=True)
         d = np.load(str(tmp_path / ("rank%d.npz" % rk)))

@@ -16,7 +16,7 @@ run() {
 }
 for s in ${STEPS:-pytest smoke bench bench5 host prof pmc issue rows}; do
   case $s in
-    pytest) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    pytest) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v -s -rf --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     bench5) run bench5 600 python bench.py --config 5 ;;
