@@ -812,15 +812,6 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
 // ---------------------------------------------------------------------------
 // decode: canonical multi-symbol decoder
 // ---------------------------------------------------------------------------
-#define HD_COUNT_ROW(LEN, LIM, FIRST, BASE) +1
-enum {  // code lengths longer than the lookup (14-bit primary set, 13-bit set)
-  NLONG = 0 HD_HUFF_LONG_CODES(HD_COUNT_ROW),
-  NLONG13 = 0 HD_HUFF_LONG_CODES13(HD_COUNT_ROW)
-};
-#undef HD_COUNT_ROW
-
-#define NLONG_PAD 16  // search width (padding rows repeat the last row)
-static_assert(NLONG <= NLONG_PAD && NLONG13 <= NLONG_PAD, "long-code search too narrow");
 // Lookup entry (tools/gen_tables.py): sym1 | L1 << 8 | cnt << 13 | sym2 << 16 | used << 27
 // (sym2 = 0 when cnt = 1).  The output bytes are bits 0..7 and 16..23 (E_OUT2):
 // the item decoder stores the second with ds_write_b8_d16_hi, no shift (round
@@ -832,19 +823,16 @@ static_assert(NLONG <= NLONG_PAD && NLONG13 <= NLONG_PAD, "long-code search too 
 #define E_USED(e) ((e) >> 27)
 #define E_OUT2 0x00FF00FFu
 #define E_OUT1 0x000000FFu
+static_assert(HD_HUFF_LONG1_N0 == 12 && HD_HUFF_LONG1_ROWS == 20, "long-code table shape");
 // The decoder's LDS tables for an LB-bit first-level lookup (14: 64 KB, the
 // most two-symbol entries; 13: 32 KB, which leaves room for more waves).
 template <int LB>
 struct DecT {
   static constexpr int BITS = LB;
-  static constexpr uint32_t NL = LB == 13 ? (uint32_t)NLONG13 : (uint32_t)NLONG;
   uint32_t lut[1 << LB];
-  uint32_t lut2[64];               // codes of LB+1..16 bits (second level)
-  uint32_t long_lim[NLONG_PAD];    // exclusive left-justified limit (last: ~0)
-  uint32_t long_delta[NLONG_PAD];  // canonical base - first code (mod 2^32)
-  uint32_t long_len[NLONG_PAD];
-  uint32_t long_n1[32];  // leading ones of a window -> its first candidate row
-  uint16_t canon[260];
+  // codes past the lookup by their leading ones (hd_huff_long1: n1 = 12..31,
+  // then the 5 bits after the first zero -> sym | len << 9)
+  uint16_t long1[HD_HUFF_LONG1_ROWS * 32];
   uint32_t depth_lo[30];
   uint16_t depth_base[30];
   uint8_t depth_ids[256];
@@ -852,7 +840,7 @@ struct DecT {
 static_assert(HD_HUFF_LUT_BITS == 14, "primary lookup");
 typedef DecT<HD_HUFF_LUT_BITS> DecTables;
 
-// (threads below `first` only meet the barriers: they may do other work,
+// (threads below `first` only meet the barrier: they may do other work,
 // e.g. the item decoder's range search, while the rest stage)
 template <int LB>
 __device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads, uint32_t first = 0) {
@@ -860,41 +848,13 @@ __device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads,
   const uint32_t t = threadIdx.x - first;  // (wraps above nthreads for threads below first)
   nthreads -= first;
   const uint32_t *lut = LB == 13 ? dev::hd_huff_lut13 : dev::hd_huff_lut;
-  const uint32_t *lut2 = LB == 13 ? dev::hd_huff_lut2_13 : dev::hd_huff_lut2;
   for (uint32_t i = t; i < (1u << LB); i += nthreads) T.lut[i] = lut[i];
-  if (t < 64) T.lut2[t] = lut2[t];
-  for (uint32_t i = t; i < 257; i += nthreads) T.canon[i] = dev::hd_huff_canon_sym[i];
+  for (uint32_t i = t; i < HD_HUFF_LONG1_ROWS * 32u; i += nthreads) T.long1[i] = dev::hd_huff_long1[i];
   if (t < 30) {
     T.depth_lo[t] = dev::hd_huff_depth_lo[t];
     T.depth_base[t] = dev::hd_huff_depth_base[t];
   }
   if (t < 256) T.depth_ids[t] = dev::hd_huff_depth_ids[t];
-  if (t == 0) {
-    uint32_t i = 0;
-#define HD_LONG_ROW(LEN, LIM, FIRST, BASE)                                    \
-    T.long_lim[i] = (LIM) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(LIM);   \
-    T.long_delta[i] = (uint32_t)(BASE) - (uint32_t)(FIRST);                  \
-    T.long_len[i] = (LEN);                                                   \
-    ++i;
-    if (LB == 13) {
-      HD_HUFF_LONG_CODES13(HD_LONG_ROW)
-    } else {
-      HD_HUFF_LONG_CODES(HD_LONG_ROW)
-    }
-#undef HD_LONG_ROW
-    for (; i < NLONG_PAD; ++i) {
-      T.long_lim[i] = 0xFFFFFFFFu;
-      T.long_delta[i] = T.long_delta[DecT<LB>::NL - 1];
-      T.long_len[i] = T.long_len[DecT<LB>::NL - 1];
-    }
-  }
-  __syncthreads();
-  if (t < 32) {  // rows below every code with t leading ones (ones, then zeros)
-    const uint32_t wmin = t ? ~0u << (32u - t) : 0u;
-    uint32_t i0 = 0;
-    for (uint32_t r = 0; r < DecT<LB>::NL; ++r) i0 += T.long_lim[r] <= wmin ? 1u : 0u;
-    T.long_n1[t] = min(i0, DecT<LB>::NL - 1u);
-  }
   __syncthreads();
 }
 
@@ -1006,31 +966,30 @@ struct CheckedDwordSink {
   }
 };
 
-// Code longer than the lookup: canonical length by a branch-free search over
-// the left-justified limits (one row per code length, padded to 16 rows),
-// then the symbol.  Returns a lookup-style entry
-// (cnt 1, used = L), or ~0u when EOS (symbol 256) completes within `rem`.
+// Code longer than the lookup: one read of the leading-ones table.  Every
+// HPACK code past 13 bits starts with n1 >= 12 ones, a zero and at most 5
+// more bits (tools/gen_tables.py long_ones_table), so (n1, those 5 bits)
+// names the code.  (Round 5; before: a second-level lookup for 14..16-bit
+// codes, then a search over the left-justified limits by leading ones and a
+// canonical-symbol read -- up to five dependent LDS reads for a 28-bit code.)
+// Returns a lookup-style entry (cnt 1, used = L), or ~0u when EOS (symbol
+// 256) completes within `rem`.
 template <class TT>
 __device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32_t rem) {
-  // the window's leading ones leave at most three candidate lengths (HPACK's
-  // codes past 16 bits): the first candidate row from long_n1, then two
-  // compares (limits are nondecreasing) -- two dependent reads, not four
-  const uint32_t n1 = min((uint32_t)__clz((int)~win), 31u);
-  uint32_t i = T.long_n1[n1];
-  const uint32_t l0 = T.long_lim[i], l1 = T.long_lim[min(i + 1u, NLONG_PAD - 1u)];
-  i += (l0 <= win ? 1u : 0u) + (l1 <= win ? 1u : 0u);
-  i = min(i, TT::NL - 1u);  // win == ~0: the 30-bit row
-  const uint32_t L = T.long_len[i];
-  const uint32_t sym = T.canon[(win >> (32 - L)) + T.long_delta[i]];
+  const uint32_t n1 = min(max((uint32_t)__clz((int)~win), (uint32_t)HD_HUFF_LONG1_N0),
+                          (uint32_t)(HD_HUFF_LONG1_N0 + HD_HUFF_LONG1_ROWS - 1));
+  // the 5 bits after the first zero: win << (n1 + 1) (alignbit: n1 = 31 gives 0)
+  const uint32_t b = __builtin_amdgcn_alignbit(win, 0u, 31u - n1) >> 27;
+  const uint32_t v = T.long1[(n1 - HD_HUFF_LONG1_N0) * 32u + b];
+  const uint32_t sym = v & 511u, L = v >> 9;
   if (L <= rem && sym == 256) return 0xFFFFFFFFu;
   return (L <= rem ? sym : 0u) | (L << 8) | (1u << 13) | (L << 27);
 }
 
-// First-level miss: the second level (codes of up to 16 bits), else the search.
+// First-level miss: the code is longer than the lookup.
 template <class TT>
 __device__ __forceinline__ uint32_t slow_entry(const TT &T, uint32_t win, uint32_t rem) {
-  const uint32_t e = T.lut2[(win >> 16) & 63u];
-  return e ? e : long_entry(T, win, rem);
+  return long_entry(T, win, rem);
 }
 
 // Decode from bit bp (positions relative to the staged round) of a string

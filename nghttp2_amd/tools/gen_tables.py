@@ -221,6 +221,37 @@ def build():
                 id_list=id_list, lut=lut, lut2=lut2, longc=longc)
 
 
+LONG1_N0 = 12    # the fewest leading ones of a code longer than 13 bits
+LONG1_ROWS = 20  # n1 = 12 .. 31 (30 and more ones: EOS)
+
+
+def long_ones_table(t):
+    """hd_huff_long1: for n1 = LONG1_N0 .. LONG1_N0 + LONG1_ROWS - 1 leading
+    ones, a zero and 5 more bits, the code that bit string starts with, as
+    sym | len << 9 (30 or more ones: EOS, len 30).  Built by matching the
+    canonical code words as bit strings."""
+    words = {}
+    codes = canonical_codes()[0]  # (code value, length) per symbol
+    for sym, (c, L) in enumerate(codes):
+        words[format(c, "0%db" % L)] = (sym, L)
+    maxlen = max(L for _, L in codes)
+    out = []
+    for r in range(LONG1_ROWS):
+        n1 = LONG1_N0 + r
+        for b in range(32):
+            bits = "1" * n1 + "0" + format(b, "05b")
+            if n1 >= 30:
+                bits = "1" * 30
+            hit = None
+            for L in range(1, min(len(bits), maxlen) + 1):
+                if bits[:L] in words:
+                    hit = words[bits[:L]]
+                    break
+            assert hit is not None and hit[1] >= 14, (n1, b, hit)
+            out.append(hit[0] | (hit[1] << 9))
+    return out
+
+
 def packed_ref_layout(t):
     """Bytes of the tables in the reference's struct layouts (for pinning):
     huff_sym_table as {u32 nbits; u32 code}, huff_decode_table as
@@ -291,6 +322,19 @@ def write_inc(t, path):
     w("#define HD_HUFF_LONG_CODES(X) \\")
     for L, lim, fc, b in t["longc"]:
         w("  X(%d, 0x%XULL, 0x%Xu, %du) \\" % (L, lim, fc, b))
+    w("")
+    lo = long_ones_table(t)
+    w("/* codes of 14..30 bits by their leading ones (round 5): a window with n1")
+    w("   leading ones (n1 >= %d, clamped to %d), then a zero, then bits b (5 of them)" % (LONG1_N0, LONG1_N0 + LONG1_ROWS - 1))
+    w("   is the code hd_huff_long1[(n1 - %d) * 32 + b] = sym | len << 9 (every code" % LONG1_N0)
+    w("   past 13 bits has n1 >= %d and at most 5 bits after its first zero; 30+" % LONG1_N0)
+    w("   ones is EOS) */")
+    w("#define HD_HUFF_LONG1_N0 %d" % LONG1_N0)
+    w("#define HD_HUFF_LONG1_ROWS %d" % LONG1_ROWS)
+    w("HD_TBL const unsigned short hd_huff_long1[%d] = {" % len(lo))
+    for i in range(0, len(lo), 16):
+        w("  " + ", ".join("0x%04X" % v for v in lo[i:i + 16]) + ",")
+    w("};")
     w("")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
