@@ -1356,6 +1356,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_SK40
 #define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)
 #endif
+#ifndef DD_SK64
+#define DD_SK64 1u  // the 64-byte instance (config 5's 30-bit codes everywhere): every pair
+#endif
 
 // Decode symbols into a byte stream in LDS: both bytes of an entry are
 // written, the count advances by the entry's symbols.
@@ -2294,7 +2297,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
   if (enc_bytes <= 48ull * n)
-    launch_decode_items<64u, DD_IW64, 13, DD_BI64, 1u, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<64u, DD_IW64, 13, DD_BI64, DD_SK64, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
     launch_decode_items<40u, DD_IW40, 13, DD_BI40, DD_SK40, DD_TS40, DD_TK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
