@@ -19,9 +19,12 @@
 //                   rounds of up to 64 items (a whole string, or a 40-byte
 //                   piece of a long one, warmed up and verified; the
 //                   64-byte instance cuts a round at an input-byte budget);
-//                   a 13-bit two-symbol lookup in LDS and a register bit
-//                   buffer; symbols through a per-lane LDS region, stored
-//                   back to back per task; the final {fstate, flags} of the
+//                   a 13-bit two-symbol lookup in LDS read through a
+//                   register window over the round's staged words, codes
+//                   past 13 bits by one read of a leading-ones table;
+//                   symbols through a per-lane LDS region, stored with
+//                   unaligned 16-byte stores back to back per task; the
+//                   final {fstate, flags} of the
 //                   reference's nibble FSM (lib/nghttp2_hd_huffman.c:122-136)
 //                   rebuilt exactly from the undecoded tail bits (DESIGN.md
 //                   "decode state")
@@ -1338,6 +1341,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_IW40
 #define DD_IW40 16
 #endif
+#ifndef DD_IP40
+#define DD_IP40 40u  // piece bytes of the long-string instance
+#endif
 #ifndef DD_TS64
 #define DD_TS64 64u  // strings per task unit of the 64-byte instance
 #endif
@@ -1385,8 +1391,6 @@ struct DIShared {  // k_decode_items
   DecT<LB> T;  // first: the lookup at LDS offset 0
   alignas(16) uint32_t ib[IW][di_ibw(di_span(IP, BI))];
   alignas(16) uint32_t ob[IW][(di_obb(IP, BI) / 4 + 1 + 3) & ~3u];
-  uint32_t ostart[IW][TASK_STR];  // string output starts (task-relative)
-  uint32_t smap[IW][WAVE];        // a round's items -> strings (1-based, max-scanned)
   uint32_t claimed, claimed1;     // tasks / tail units of the workgroup's range claimed so far
   uint32_t range[2];              // the workgroup's task range (wave 0's search)
   uint8_t tperm[64];              // claim order of the range's tail units (largest first)
@@ -1733,7 +1737,6 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   // (budgeted rounds: the lane's output region moves with the round)
   lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
-  lds_u32 *ost = (lds_u32 *)S.ostart[wv];
   if (threadIdx.x == 0) {
     S.claimed = 0u;
     S.claimed1 = 0u;
@@ -1748,7 +1751,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   // (encoded bytes + DD_TASK_W per string) over the grid, its waves striding
   // over it (config 3: 348 vs 356 us); else the grid strides over all tasks
   // (the search costs a short batch more than it saves)
-  constexpr bool kBal = IP == 40u;
+  constexpr bool kBal = IP < 64u;
   uint32_t t_lo, t_hi;
   {
     const uint32_t nwg = gridDim.x, g = blockIdx.x;
@@ -1900,7 +1903,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     const uint32_t P_l = wave_incl_scan(m_l), X_l = P_l - m_l;
     const uint32_t M = __builtin_amdgcn_readlane(P_l, 63);
     uint32_t carry_exit = DD_NONE, carry_cnt = 0, IB_prev = 0, run = 0;
-    lds_u32 *smap = (lds_u32 *)S.smap[wv];
+    uint32_t ost_me = 0;  // string `lane`'s output start (task-relative)
     uint32_t R0 = A;
     for (uint32_t r0 = 0, nv = 0; r0 < M; r0 += nv) {
       nv = min(M - r0, (uint32_t)WAVE);  // (budgeted rounds: cut below)
@@ -1911,15 +1914,19 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // (a task of single-item strings: item = string, no map)
       uint32_t i = lane, k = 0, a = a_l, b = b_l;
       if (M != nstr) {
-        smap[lane] = 0u;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (sl && P_l > r0 && X_l < r0 + WAVE) smap[X_l > r0 ? X_l - r0 : 0u] = lane + 1u;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        i = min(wave_incl_max(smap[lane]), nstr) - 1u;
+        // every string with an item in the round marks the lane of its first
+        // one (or lane 0); item q's string is the last mark at or below q:
+        // the first marked string plus the marks in lanes 1..q (round 5: an
+        // OR over the wave instead of an LDS map and a max-scan, which frees
+        // the map's 4 KB per workgroup)
+        const bool mk = sl && P_l > r0 && X_l < r0 + WAVE;
+        const uint32_t pos = X_l > r0 ? X_l - r0 : 0u;
+        const uint32_t mlo = wave_or(mk && pos < 32u ? 1u << pos : 0u);
+        const uint32_t mhi = wave_or(mk && pos >= 32u ? 1u << (pos - 32u) : 0u);
+        const uint64_t heads = ((uint64_t)mhi << 32) | mlo;
+        const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(mk));
+        const uint32_t c = (uint32_t)__builtin_popcountll(heads & (~0ull >> (63u - lane)));
+        i = min(first + c, nstr) - 1u;
         k = q - __shfl(X_l, i, 64);
         a = __shfl(a_l, i, 64);
         b = __shfl(b_l, i, 64);
@@ -2076,9 +2083,14 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         dd_finish(S.T, rr.failed, rr.t, rr.win, seg,
                   task_ovf && auto_slot(b - off0, t0 + i + 1u) > dst_cap, t0 + i, status,
                   fstate_out, flags_out);
-      // ---- dense placement
+      // ---- dense placement; a string whose first item is in the round
+      // takes its output start from that item's lane
       const uint32_t O_l = run + Tinc - V;
-      if (valid && k == 0) ost[i] = O_l;
+      {
+        const uint32_t fq = X_l - r0;  // (wraps for strings that started earlier)
+        const uint32_t got = __shfl(O_l, fq & 63u, 64);
+        if (sl && X_l >= r0 && fq < nv) ost_me = got;
+      }
       // ---- store: each lane stores its region straight to its output bytes
       // with unaligned stores (gfx950 global memory takes them whole):
       // 16-byte pieces, then the tail as 8-, 4-, 2- and 1-byte pieces.
@@ -2135,7 +2147,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     }
     // ---- epilogue: output starts
     if (sl) {
-      dst_off[t0 + lane] = (uint32_t)min(tbase + ost[lane], dst_cap);
+      dst_off[t0 + lane] = (uint32_t)min(tbase + ost_me, dst_cap);
       if (t0 + lane == n - 1u) dst_off[n] = (uint32_t)min(tbase + run, dst_cap);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2299,7 +2311,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if (enc_bytes <= 48ull * n)
     launch_decode_items<64u, DD_IW64, 13, DD_BI64, DD_SK64, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
-    launch_decode_items<40u, DD_IW40, 13, DD_BI40, DD_SK40, DD_TS40, DD_TK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<DD_IP40, DD_IW40, 13, DD_BI40, DD_SK40, DD_TS40, DD_TK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
 }
 

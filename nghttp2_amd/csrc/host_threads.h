@@ -44,23 +44,37 @@ class Pool {
   }
   unsigned workers() const { return (unsigned)th_.size(); }
   // Runs fn on every worker and on the caller; returns when all are done.
-  // Calls from several host threads take turns.
+  // Calls from several host threads take turns.  Workers spin for a short
+  // while (spin_us()) after each job before they park on the condition
+  // variable, so the several parallel phases of one front-end call hand
+  // work over without a futex wake-up each (round 5: the inflate call runs
+  // five such phases in well under a millisecond).
   void run(const std::function<void()> &fn) {
     std::lock_guard<std::mutex> turn(run_mu_);
+    job_.store(&fn, std::memory_order_relaxed);
+    active_.store((unsigned)th_.size(), std::memory_order_relaxed);
+    bool wake;
     {
       std::lock_guard<std::mutex> l(mu_);
-      job_ = &fn;
-      active_ = (unsigned)th_.size();
-      ++gen_;
+      gen_.fetch_add(1, std::memory_order_release);
+      wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
     fn();
-    std::unique_lock<std::mutex> l(mu_);
-    done_.wait(l, [&] { return active_ == 0; });
-    job_ = nullptr;
+    for (unsigned i = 0; active_.load(std::memory_order_acquire) != 0; ++i)
+      if (i > 4096) std::this_thread::yield();
+    job_.store(nullptr, std::memory_order_relaxed);
   }
 
  private:
+  // NGHTTP2_AMD_SPIN_US (default 200; 0: park at once, as before round 5)
+  static int spin_us() {
+    static const int v = [] {
+      const char *e = getenv("NGHTTP2_AMD_SPIN_US");
+      return e ? std::max(0, atoi(e)) : 200;
+    }();
+    return v;
+  }
   explicit Pool(unsigned n) {
     for (unsigned k = 0; k < n; ++k) {
       try {
@@ -74,24 +88,36 @@ class Pool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      const std::function<void()> *j;
-      {
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return gen_ != seen; });
-        seen = gen_;
-        j = job_;
+      // spin for the next job for kSpinUs, then park
+      bool got = false;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned i = 0; !got; ++i) {
+        if (gen_.load(std::memory_order_acquire) != seen) {
+          got = true;
+          break;
+        }
+        if ((i & 255u) == 255u &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us()))
+          break;
       }
-      (*j)();
-      std::lock_guard<std::mutex> l(mu_);
-      if (--active_ == 0) done_.notify_all();
+      if (!got) {
+        std::unique_lock<std::mutex> l(mu_);
+        ++sleepers_;
+        cv_.wait(l, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+        --sleepers_;
+      }
+      seen = gen_.load(std::memory_order_acquire);
+      (*job_.load(std::memory_order_relaxed))();
+      active_.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
   std::vector<std::thread> th_;
   std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void()> *job_ = nullptr;
-  unsigned active_ = 0;
-  uint64_t gen_ = 0;
+  std::condition_variable cv_;
+  std::atomic<const std::function<void()> *> job_{nullptr};
+  std::atomic<unsigned> active_{0};
+  std::atomic<uint64_t> gen_{0};
+  unsigned sleepers_ = 0;  // (under mu_)
 };
 
 // f(i) for i in [0, n), `grain` consecutive indices per fetch; serial when

@@ -214,10 +214,73 @@ def bench_inflate(nconn=256, per_conn=8, fields=16, reps=5, index=False):
                     "inflate_blocks wrapper, Python marshalling in and out included" % (3 * reps)}
 
 
+def bench_inflate_alt(nconn=256, per_conn=8, fields=16, alternations=7, index=False):
+    """The batched inflate front-end's C call against the 16-thread CPU port
+    of the same inflater (oracle/hpack_inflate_oracle.c) on the same blocks,
+    in one process, alternating: each alternation times 5 front-end calls and
+    3 CPU-port runs and keeps the median of each; the row reports the
+    medians over the alternations and their ratio (the host threads are a
+    share of a larger machine and swing between runs, so neither side is
+    timed in isolation)."""
+    import ctypes
+    import statistics
+    import nghttp2_amd
+    from nghttp2_amd import hd
+    from oracle import hpack_oracle as HO
+    blocks, conns = make_blocks(nconn, per_conn, fields, index=index)
+    wire = sum(len(b) for b in blocks)
+    L = hd._inflate_lib()
+    m = len(blocks)
+    keep = [ctypes.create_string_buffer(b, len(b)) for b in blocks]
+    ptrs = (ctypes.c_void_p * m)(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+    lens = (ctypes.c_size_t * m)(*[len(b) for b in blocks])
+    nva_cap, arena_cap = wire + 16, 8 * wire + 4096
+    nva = (hd._Nv * nva_cap)()
+    arena = (ctypes.c_uint8 * arena_cap)()
+    stc = (ctypes.c_int32 * m)()
+    nv_used, ar_used = ctypes.c_size_t(), ctypes.c_size_t()
+    import torch
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+    ip = (ctypes.c_void_p * m)(*[infs[c].p.value for c in conns])
+    nf = None
+    gpu_med, cpu_med = [], []
+    for a in range(alternations):
+        ts = []
+        for _ in range(5):
+            if index:
+                fresh = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+                ip = (ctypes.c_void_p * m)(*[fresh[c].p.value for c in conns])
+            t0 = time.perf_counter()
+            rv = L.nghttp2_amd_hd_inflate_blocks(ip, m, ptrs, lens, nva, nva_cap, ctypes.byref(nv_used),
+                                                 arena, arena_cap, ctypes.byref(ar_used), stc, s)
+            ts.append(time.perf_counter() - t0)
+            assert rv == 0
+            nf = nv_used.value if nf is None else nf
+            assert nv_used.value == nf
+        gpu_med.append(statistics.median(ts))
+        cs = []
+        for _ in range(3):
+            dt, nfc = HO.c_inflate_batch_timed(blocks, conns, nconn, 16)
+            assert nfc == nf
+            cs.append(dt)
+        cpu_med.append(statistics.median(cs))
+    g, c = statistics.median(gpu_med), statistics.median(cpu_med)
+    return {"blocks": m, "connections": nconn, "fields": nf, "wire_bytes": wire,
+            "incremental_indexing": index, "alternations": alternations,
+            "c_s_per_call_median": round(g, 6), "c_wire_MBps": round(wire / g / 1e6, 1),
+            "cpu_port_16t_s_median": round(c, 6), "cpu_port_16t_wire_MBps": round(wire / c / 1e6, 1),
+            "ratio_front_end_over_cpu16": round(c / g, 3),
+            "per_alternation_c_s": [round(x, 6) for x in gpu_med],
+            "per_alternation_cpu16_s": [round(x, 6) for x in cpu_med]}
+
+
 if __name__ == "__main__":
     rows = sys.argv[1:] or ["emit", "emit3", "inflate", "names"]
     fns = {"emit": bench_emit, "emit3": lambda: bench_emit(cfg=3), "inflate": bench_inflate,
            "inflate_index": lambda: bench_inflate(index=True),
+           "inflate_alt": bench_inflate_alt,
+           "inflate_alt_index": lambda: bench_inflate_alt(index=True),
            "names": bench_names,
            "names_short": lambda: bench_names(long_frac=0.0)}
     print(json.dumps({r: fns[r]() for r in rows}, indent=1))
