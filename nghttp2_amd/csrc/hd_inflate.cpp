@@ -216,8 +216,10 @@ struct BlockOut {
 
 struct Engine {
   std::mutex mu;
-  uint8_t *h_pool = nullptr;  // pinned: Huffman literals in, decoded out
+  uint8_t *h_pool = nullptr;  // pinned: Huffman literals in
   size_t h_cap = 0;
+  uint8_t *h_out = nullptr;  // pinned: decoded literals out
+  size_t o_cap = 0;
   uint32_t *h_meta = nullptr;  // pinned: offsets in, slots + status out
   size_t m_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -229,7 +231,6 @@ struct Engine {
   std::vector<Block> bl;
   std::vector<uint32_t> nhuff;
   std::vector<uint64_t> hbytes;
-  std::vector<const Lit *> huff;
   std::vector<uint32_t> hoff;
   uint64_t gen = 0;  // inflate_blocks calls (the connections' grouping stamp)
   std::vector<nghttp2_amd_hd_inflater *> conns;
@@ -246,12 +247,14 @@ bool hip_ok(hipError_t e, const char *what) {
   return false;
 }
 
+// (pinned, mapped into the device's address space and coherent: the
+// zero-copy decode reads and writes these pools directly)
 bool grow_host(void **p, size_t *cap, size_t need) {
   if (need <= *cap) return true;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
-  if (!hip_ok(hipHostMalloc(p, need, hipHostMallocDefault), "hipHostMalloc")) return false;
+  if (!hip_ok(hipHostMalloc(p, need, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc")) return false;
   *cap = need;
   return true;
 }
@@ -640,11 +643,39 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   if (E.hbytes[nblocks] > UINT32_MAX ||
       (nh && nghttp2_amd_hd_huff_decode_bound(E.hbytes[nblocks], nh) > UINT32_MAX))
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
-  if (E.huff.size() < nh) E.huff.resize(nh);
   if (E.hoff.size() < (size_t)nh + 1) E.hoff.resize((size_t)nh + 1);
-  std::vector<const Lit *> &huff = E.huff;
   std::vector<uint32_t> &hoff = E.hoff;
+  // ---- GPU: every Huffman literal of the batch in one decode.  The pinned
+  // pools are sized first, so each block numbers its literals and copies
+  // their bytes into the pinned input pool in one parallel pass (round 5;
+  // before: numbering, then a separate gather over the literals).  By
+  // default the kernel reads the literals and offsets straight from the
+  // mapped pinned pools (zero-copy in: no H2D copies or their launch
+  // latencies) and its output is copied out;  NGHTTP2_AMD_INFLATE_ZC=1 also
+  // writes the output through the mapped pool, 0 copies both ways.
+  // (2: zero-copy in, the output copied out -- DMA lands it in whole lines)
+  static const int zc_mode = [] {
+    const char *e = getenv("NGHTTP2_AMD_INFLATE_ZC");
+    return e ? atoi(e) : 2;
+  }();
+  const bool zero_copy = zc_mode == 1, zero_in = zc_mode == 2;
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t hb = E.hbytes[nblocks];
+  const size_t in_bytes = ((size_t)hb + 15u) / 16u * 16u + 16u;
+  const size_t out_bytes = nh ? nghttp2_amd_hd_huff_decode_bound(hb, nh) : 0;
+  const size_t meta = 3u * ((size_t)nh + 1u) * sizeof(uint32_t);
+  if (nh) {
+    if (!grow_host((void **)&E.h_pool, &E.h_cap, in_bytes) ||
+        !grow_host((void **)&E.h_out, &E.o_cap, out_bytes) ||
+        !grow_host((void **)&E.h_meta, &E.m_cap, meta))
+      return NGHTTP2_AMD_ERR_NOMEM;
+    if (!zero_copy && ((!zero_in && !grow_dev((void **)&E.d_in, &E.din_cap, in_bytes)) ||
+                       !grow_dev((void **)&E.d_out, &E.dout_cap, out_bytes) ||
+                       !grow_dev((void **)&E.d_off, &E.dn_cap, meta)))
+      return NGHTTP2_AMD_ERR_NOMEM;
+  }
   hoff[0] = 0;
+  uint8_t *const hp = E.h_pool;
   parallel_for(nblocks, 64, [&](size_t i) {  // each block numbers and places its literals
     uint32_t k = nhuff[i];
     uint32_t o = (uint32_t)E.hbytes[i];
@@ -652,13 +683,13 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       if (op.kind != Op::LITERAL) continue;
       if (op.name.huff == 0) {
         op.name.huff = (int32_t)k;
-        huff[k] = &op.name;
+        memcpy(hp + o, op.name.p, op.name.len);
         o += op.name.len;
         hoff[++k] = o;
       }
       if (op.val.huff == 0) {
         op.val.huff = (int32_t)k;
-        huff[k] = &op.val;
+        memcpy(hp + o, op.val.p, op.val.len);
         o += op.val.len;
         hoff[++k] = o;
       }
@@ -666,50 +697,61 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   });
 
   ph.mark("parse");
-  // ---- GPU: every Huffman literal of the batch in one decode
   const uint8_t *dec = nullptr;
   const uint32_t *slot = nullptr;
   const int32_t *hst = nullptr;
   if (nh) {
-    hipStream_t st = (hipStream_t)stream;
-    const size_t in_bytes = ((size_t)hoff[nh] + 15u) / 16u * 16u + 16u;
-    const size_t out_bytes = nghttp2_amd_hd_huff_decode_bound(hoff[nh], nh);
-    const size_t meta = 3u * ((size_t)nh + 1u) * sizeof(uint32_t);
-    if (!grow_host((void **)&E.h_pool, &E.h_cap, in_bytes > out_bytes ? in_bytes : out_bytes) ||
-        !grow_host((void **)&E.h_meta, &E.m_cap, meta) ||
-        !grow_dev((void **)&E.d_in, &E.din_cap, in_bytes) ||
-        !grow_dev((void **)&E.d_out, &E.dout_cap, out_bytes) ||
-        !grow_dev((void **)&E.d_off, &E.dn_cap, meta))
-      return NGHTTP2_AMD_ERR_NOMEM;
-    E.d_slot = E.d_off + (nh + 1);
-    E.d_st = (int32_t *)(E.d_slot + (nh + 1));
-    parallel_for(nh, 4096, [&](size_t k) { memcpy(E.h_pool + hoff[k], huff[k]->p, huff[k]->len); });
-    memset(E.h_pool + hoff[nh], 0, in_bytes - hoff[nh]);
+    memset(E.h_pool + hb, 0, in_bytes - hb);
     memcpy(E.h_meta, hoff.data(), (nh + 1) * sizeof(uint32_t));
-    // a failure after the first copy is queued drains the stream before
-    // returning: a copy still in flight must not land in the pinned pool
-    // after the next call has filled it
+    uint32_t *h_slot = E.h_meta + (nh + 1);
+    int32_t *h_st = (int32_t *)(h_slot + (nh + 1));
+    // a failure after the first copy or launch is queued drains the stream
+    // before returning: GPU work still in flight must not land in the pinned
+    // pools after the next call has filled them
     auto drain = [st](int rv) {
       (void)hipStreamSynchronize(st);
       return rv;
     };
-    if (hipMemcpyAsync(E.d_in, E.h_pool, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(E.d_off, E.h_meta, (nh + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                       st) != hipSuccess)
-      return drain(NGHTTP2_AMD_ERR_FATAL);
-    int rv = nghttp2_amd_hd_huff_decode_batch_auto(E.d_in, E.d_off, nh, (uint64_t)hoff[nh], E.d_out,
-                                                   out_bytes, E.d_slot, E.d_st, nullptr, nullptr,
-                                                   stream);
-    if (rv) return drain(rv);
-    uint32_t *h_slot = E.h_meta + (nh + 1);
-    int32_t *h_st = (int32_t *)(h_slot + (nh + 1));
-    if (hipMemcpyAsync(E.h_pool, E.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_slot, E.d_slot, (nh + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                       st) != hipSuccess ||
-        hipMemcpyAsync(h_st, E.d_st, nh * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
-            hipSuccess)
-      return drain(NGHTTP2_AMD_ERR_FATAL);
-    dec = E.h_pool;
+    if (zero_copy) {
+      void *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr;
+      if (hipHostGetDevicePointer(&d_in, E.h_pool, 0) != hipSuccess ||
+          hipHostGetDevicePointer(&d_out, E.h_out, 0) != hipSuccess ||
+          hipHostGetDevicePointer(&d_meta, E.h_meta, 0) != hipSuccess)
+        return NGHTTP2_AMD_ERR_FATAL;
+      uint32_t *d_off = (uint32_t *)d_meta;
+      int rv = nghttp2_amd_hd_huff_decode_batch_auto((const uint8_t *)d_in, d_off, nh, hb, (uint8_t *)d_out,
+                                                     out_bytes, d_off + (nh + 1),
+                                                     (int32_t *)(d_off + 2 * (nh + 1)), nullptr, nullptr,
+                                                     stream);
+      if (rv) return drain(rv);
+    } else {
+      E.d_slot = E.d_off + (nh + 1);
+      E.d_st = (int32_t *)(E.d_slot + (nh + 1));
+      const uint8_t *src = E.d_in;
+      const uint32_t *src_off = E.d_off;
+      if (zero_in) {  // the kernel reads the literals and offsets from the pinned pools
+        void *d_in = nullptr, *d_meta = nullptr;
+        if (hipHostGetDevicePointer(&d_in, E.h_pool, 0) != hipSuccess ||
+            hipHostGetDevicePointer(&d_meta, E.h_meta, 0) != hipSuccess)
+          return NGHTTP2_AMD_ERR_FATAL;
+        src = (const uint8_t *)d_in;
+        src_off = (const uint32_t *)d_meta;
+      } else if (hipMemcpyAsync(E.d_in, E.h_pool, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+                 hipMemcpyAsync(E.d_off, E.h_meta, (nh + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                st) != hipSuccess) {
+        return drain(NGHTTP2_AMD_ERR_FATAL);
+      }
+      int rv = nghttp2_amd_hd_huff_decode_batch_auto(src, src_off, nh, hb, E.d_out, out_bytes,
+                                                     E.d_slot, E.d_st, nullptr, nullptr, stream);
+      if (rv) return drain(rv);
+      if (hipMemcpyAsync(E.h_out, E.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(h_slot, E.d_slot, (nh + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         st) != hipSuccess ||
+          hipMemcpyAsync(h_st, E.d_st, nh * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+              hipSuccess)
+        return drain(NGHTTP2_AMD_ERR_FATAL);
+    }
+    dec = E.h_out;
     slot = h_slot;
     hst = h_st;
   }
