@@ -826,6 +826,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
 #define E_USED(e) ((e) >> 27)
 #define E_OUT2 0x00FF00FFu
 #define E_OUT1 0x000000FFu
+#define E_EOS 0x00008000u  // (long-code entries only) the code is EOS
 static_assert(HD_HUFF_LONG1_N0 == 12 && HD_HUFF_LONG1_ROWS == 20, "long-code table shape");
 // The decoder's LDS tables for an LB-bit first-level lookup (14: 64 KB, the
 // most two-symbol entries; 13: 32 KB, which leaves room for more waves).
@@ -834,8 +835,9 @@ struct DecT {
   static constexpr int BITS = LB;
   uint32_t lut[1 << LB];
   // codes past the lookup by their leading ones (hd_huff_long1: n1 = 12..31,
-  // then the 5 bits after the first zero -> sym | len << 9)
-  uint16_t long1[HD_HUFF_LONG1_ROWS * 32];
+  // then the 5 bits after the first zero), staged as lookup entries (one
+  // symbol, used = its length) with E_EOS for the 30-bit EOS code
+  uint32_t long1[HD_HUFF_LONG1_ROWS * 32];
   uint32_t depth_lo[30];
   uint16_t depth_base[30];
   uint8_t depth_ids[256];
@@ -852,7 +854,10 @@ __device__ __forceinline__ void stage_dec_tables(DecT<LB> &T, uint32_t nthreads,
   nthreads -= first;
   const uint32_t *lut = LB == 13 ? dev::hd_huff_lut13 : dev::hd_huff_lut;
   for (uint32_t i = t; i < (1u << LB); i += nthreads) T.lut[i] = lut[i];
-  for (uint32_t i = t; i < HD_HUFF_LONG1_ROWS * 32u; i += nthreads) T.long1[i] = dev::hd_huff_long1[i];
+  for (uint32_t i = t; i < HD_HUFF_LONG1_ROWS * 32u; i += nthreads) {
+    const uint32_t v = dev::hd_huff_long1[i], sym = v & 511u, L = v >> 9;
+    T.long1[i] = (sym & 255u) | (L << 8) | (1u << 13) | (L << 27) | (sym == 256u ? E_EOS : 0u);
+  }
   if (t < 30) {
     T.depth_lo[t] = dev::hd_huff_depth_lo[t];
     T.depth_base[t] = dev::hd_huff_depth_base[t];
@@ -977,16 +982,21 @@ struct CheckedDwordSink {
 // canonical-symbol read -- up to five dependent LDS reads for a 28-bit code.)
 // Returns a lookup-style entry (cnt 1, used = L), or ~0u when EOS (symbol
 // 256) completes within `rem`.
+__device__ __forceinline__ uint32_t long_index(uint32_t win);
 template <class TT>
 __device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32_t rem) {
+  // (n1 leading ones, clamped to 12..31, then the 5 bits after the first
+  // zero: win << (n1 + 1), by alignbit so that n1 = 31 gives 0)
+  const uint32_t v = T.long1[long_index(win)];
+  const uint32_t L = E_USED(v);
+  if (L <= rem && (v & E_EOS)) return 0xFFFFFFFFu;
+  return L <= rem ? v & ~E_EOS : v & ~(E_EOS | 0xFFu);
+}
+// The index of a window's code in T.long1 (long_entry's read).
+__device__ __forceinline__ uint32_t long_index(uint32_t win) {
   const uint32_t n1 = min(max((uint32_t)__clz((int)~win), (uint32_t)HD_HUFF_LONG1_N0),
                           (uint32_t)(HD_HUFF_LONG1_N0 + HD_HUFF_LONG1_ROWS - 1));
-  // the 5 bits after the first zero: win << (n1 + 1) (alignbit: n1 = 31 gives 0)
-  const uint32_t b = __builtin_amdgcn_alignbit(win, 0u, 31u - n1) >> 27;
-  const uint32_t v = T.long1[(n1 - HD_HUFF_LONG1_N0) * 32u + b];
-  const uint32_t sym = v & 511u, L = v >> 9;
-  if (L <= rem && sym == 256) return 0xFFFFFFFFu;
-  return (L <= rem ? sym : 0u) | (L << 8) | (1u << 13) | (L << 27);
+  return (n1 - HD_HUFF_LONG1_N0) * 32u + (__builtin_amdgcn_alignbit(win, 0u, 31u - n1) >> 27);
 }
 
 // First-level miss: the code is longer than the lookup.
@@ -1362,6 +1372,15 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_SK40
 #define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)
 #endif
+#ifndef DD_DIRECT_MODE
+#define DD_DIRECT_MODE 1  // dd_run's direct long codes (SLOWK == 1) when the caller asks: 0 never
+#endif
+#ifndef DD_DIRECT_MIN
+#define DD_DIRECT_MIN 4u  // lanes of a round with long codes that switch the wave's next round to direct
+#endif
+#ifndef DD_DIRECT_KEEP
+#define DD_DIRECT_KEEP 4u  // ... and to keep it on for the round after
+#endif
 #ifndef DD_SK64
 #define DD_SK64 1u  // the 64-byte instance (config 5's 30-bit codes everywhere): every pair
 #endif
@@ -1482,7 +1501,8 @@ struct DDRun {
 template <class Sink, bool SYNC = false, bool PAIRS = false, uint32_t SLOWK = 1, class TT, class IN>
 __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
                                         uint32_t bstop, uint32_t bend, Sink &sink,
-                                        int32_t lim = INT32_MAX) {
+                                        int32_t lim = INT32_MAX, bool direct = false,
+                                        uint32_t *nslow = nullptr) {
   DDRun r;
   r.at_end = false;
   r.t = 0;
@@ -1534,31 +1554,64 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
     const uint32_t U_ = E_USED(ek_);                                     \
     if (SYNC) ls = U_;                                                   \
     DD_ADV(U_);                                                          \
+    if (nslow) ++*nslow;                                                 \
   } while (0)
   // The fast pairs run at raised wave priority: the SIMD issues their
   // dependent chain's VALU before other waves' staging, scans and stores
   // (config 3 decode 294.1 vs 297.7 us, config 2 50.6 vs 52.2; priority 3,
   // or priority over the whole run with its careful steps: no better)
-  uint32_t it = 0;
-  __builtin_amdgcn_s_setprio(1);
-  while ((int32_t)nq >= nG) {
-    const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
-    const uint32_t e1 = T.lut[w >> (32 - TT::BITS)];
-    const uint32_t U1 = E_USED(e1);
-    const uint32_t e2 = T.lut[(w << U1) >> (32 - TT::BITS)];
-    sink.put2(e1, e2);
-    const uint32_t U2 = E_USED(e2);
-    if (SYNC) {
-      pb = nq;  // (as bp after the loop)
-      le1 = e1;
-      le2 = e2;
-      ls = 0;
+  // direct (the 64-byte instance only, SLOWK == 1, chosen per round by the
+  // caller: a wave whose last round met many long codes, as config 5's
+  // strings of 28- and 30-bit codes do): a window whose first code is past
+  // the lookup (e1 = 0) reads that code from the leading-ones table as the
+  // pair's second read (its address computed while e1 is in flight), so the
+  // pair decodes it instead of stalling for the slow path; a long code that
+  // would pass the string end, or EOS, stops the lane for the careful
+  // steps.  (Round 5: always on it took config 5 from 103.5 to 94.2 us but
+  // config 2, which has no such codes, from 41.6 to 47.4; behind a wave
+  // ballot per pair 97.5 / 43.8.  The loop is compiled both ways; the
+  // caller switches a wave per round by the count of long codes its lanes
+  // met (*nslow: slow-path runs plus direct decodes): sticky per wave,
+  // config 2 +0.8 us; per round, on at 4 lanes and kept at 4, config 5
+  // 100.9 -> 96.4 with config 2 41.7 -> 41.9, one box, 16 rounds each.)
+  uint32_t it = 0, nlong = 0;
+  auto pairs = [&](auto dir) {
+    constexpr bool kDirect = decltype(dir)::value;
+    while ((int32_t)nq >= nG) {
+      const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
+      const uint32_t e1 = T.lut[w >> (32 - TT::BITS)];
+      const uint32_t U1 = E_USED(e1);
+      uint32_t e2;
+      if (kDirect) {
+        const uint32_t li = long_index(w);
+        const uint32_t *p2 = e1 ? &T.lut[(w << U1) >> (32 - TT::BITS)] : &T.long1[li];
+        e2 = *p2;
+        const bool bad = e1 == 0u && ((e2 & E_EOS) || E_USED(e2) > bend - (~nq + 1u));
+        e2 = bad ? 0u : e2;
+        nG = bad ? INT32_MAX : nG;
+        nlong += e1 == 0u ? 1u : 0u;
+      } else {
+        e2 = T.lut[(w << U1) >> (32 - TT::BITS)];
+      }
+      sink.put2(e1, e2);
+      const uint32_t U2 = E_USED(e2);
+      if (SYNC) {
+        pb = nq;  // (as bp after the loop)
+        le1 = e1;
+        le2 = e2;
+        ls = 0;
+      }
+      DD_ADV(U1 + U2);
+      ++it;
+      if ((SLOWK == 1u || (it & (SLOWK - 1u)) == 0u) && e2 == 0u && (!kDirect || e1 != 0u))
+        DD_SLOW(); /* (an e1 of 0 stalls e2 too; direct: e1 = 0 was decoded or stopped) */
     }
-    DD_ADV(U1 + U2);
-    ++it;
-    if ((SLOWK == 1u || (it & (SLOWK - 1u)) == 0u) && e2 == 0u) DD_SLOW(); /* (an e1 of 0 stalls e2 too) */
-  }
+  };
+  __builtin_amdgcn_s_setprio(1);
+  if (SLOWK == 1u && DD_DIRECT_MODE != 0 && direct) pairs(std::true_type{});
+  else pairs(std::false_type{});
   __builtin_amdgcn_s_setprio(0);
+  if (nslow) *nslow += nlong;
 #undef DD_SLOW
   bp = ~nq + 1u;
   if (SYNC && !failed && (int32_t)bp >= (int32_t)bstop) {
@@ -1875,6 +1928,12 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   uint32_t task_k = next_k;
   load_offs(t_first < t_hi ? t_first : ntask, task_k, na_l, nb_l);
   uint32_t next_task = t_hi;
+  // direct long codes (the 64-byte instance, see dd_run): on for the wave's
+  // next round when DD_DIRECT_MIN of this round's lanes met a code past the
+  // lookup (slow-path runs, or direct decodes of such codes; DD_DIRECT_KEEP
+  // of them to stay on)
+  bool dmode = false;
+  uint32_t nslow = 0;
   for (uint32_t task = t_first; task < t_hi;) {
     next_task = claim_next(task);
     const uint32_t t0 = task * TS;
@@ -2013,7 +2072,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       if (spec) {
         uint32_t bp = 8u * (s - DD_OV - IBX);
         DiscardSink dk;
-        const DDRun rw = dd_run<DiscardSink, true, false, SK>(S.T, inp, bp, bs, bend, dk);
+        const DDRun rw = dd_run<DiscardSink, true, false, SK>(S.T, inp, bp, bs, bend, dk, INT32_MAX,
+                                                              dmode, &nslow);
         entry = bp;
         dead = rw.failed;
       }
@@ -2025,7 +2085,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       // (kMerge: the item is decoded in the verify loop's first pass, by the
       // same inlined decoder as its re-decodes)
       constexpr bool kMerge = BI == 0;
-      if (valid && !dead && !kMerge) rr = dd_run<DISink, false, false, SK>(S.T, inp, bp, bstop, bend, sk);
+      if (valid && !dead && !kMerge)
+        rr = dd_run<DISink, false, false, SK>(S.T, inp, bp, bstop, bend, sk, INT32_MAX, dmode, &nslow);
       uint32_t my_exit = rr.failed ? XFAIL : bp;
       uint32_t my_entry = dead ? XUNKNOWN : entry;
       uint32_t c0 = sk.count();
@@ -2039,7 +2100,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
           if (run_) {
             DISink s3(my_ob);
             uint32_t bq = start;
-            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3);
+            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3, INT32_MAX, dmode, &nslow);
             my_exit = rr.failed ? XFAIL : bq;
             c0 = s3.count();
           }
@@ -2064,12 +2125,17 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
             run_ = true;
           } else {
             uint32_t bq = pred;
-            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3);
+            rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3, INT32_MAX, dmode, &nslow);
             my_exit = rr.failed ? XFAIL : bq;
             c0 = s3.count();
           }
           my_entry = pred;
         }
+      }
+      if (SK == 1u && DD_DIRECT_MODE != 0) {
+        dmode = __builtin_popcountll(__ballot(nslow != 0u)) >=
+                (dmode ? DD_DIRECT_KEEP : DD_DIRECT_MIN);
+        nslow = 0;
       }
       // ---- string symbol counts: segmented scan (heads: first items)
       // (the plain inclusive scan of the lanes' byte counts, less its value
