@@ -503,7 +503,49 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   __shared__ uint32_t o_sh[WG + 1];
   __shared__ uint32_t red[2 * (WG / 64)];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  codeT[threadIdx.x] = make_uint2(dev::hd_huff_enc_code[threadIdx.x], dev::hd_huff_enc_len[threadIdx.x]);
+  // every load of the prologue is issued before any is used, so a tile's
+  // start costs one memory latency (round 5: the staging, the offsets, the
+  // tile sums and the tile's own sum waited in turn)
+  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
+  const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
+  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
+  const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
+  const bool sl = lane < nstr;
+  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
+  const uint32_t tsum = tile_sums[blockIdx.x];
+  const uint32_t cc = dev::hd_huff_enc_code[threadIdx.x], cl = dev::hd_huff_enc_len[threadIdx.x];
+  // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
+  // strings, L2-resident), in 64 bits (a batch's encoded total may pass the
+  // uint32 offset range); pre is each thread's part of the sum the block
+  // scans add up.  Thread t sums tiles [16 t, 16 t + 16) of each 4096 before
+  // this one with four 16-byte loads issued together (round 5: a strided
+  // loop that waited for each load in turn, 29 % of a wave's time on config
+  // 3 by the stamps)
+  uint64_t pre = 0;
+  const uint32_t bt = blockIdx.x;
+  const bool vec = tile_pre == nullptr && ((uintptr_t)tile_sums & 15u) == 0;
+  uint4 v[4];
+  auto batch_load = [&](uint32_t base) {
+    const uint32_t q0 = base + 16u * threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k)
+      v[k] = q0 + 4u * k < bt ? reinterpret_cast<const uint4 *>(tile_sums)[(q0 >> 2) + k] : make_uint4(0, 0, 0, 0);
+  };
+  auto batch_sum = [&](uint32_t base) {
+    const uint32_t q0 = base + 16u * threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+      const uint32_t i = q0 + 4u * k;  // (the 16 bytes may reach 3 tiles past bt: masked)
+      pre += (uint64_t)(i < bt ? v[k].x : 0u) + (i + 1u < bt ? v[k].y : 0u) +
+             (uint64_t)(i + 2u < bt ? v[k].z : 0u) + (i + 3u < bt ? v[k].w : 0u);
+    }
+  };
+  if (tile_pre) {  // a large batch: the prefixes were scanned by k_tile_prefix64
+    pre = threadIdx.x == 0 ? tile_pre[bt] : 0u;
+  } else if (vec) {
+    batch_load(0u);
+  }
+  codeT[threadIdx.x] = make_uint2(cc, cl);
   lds_u32 *img = (lds_u32 *)image[wv];
   for (uint32_t i = lane; i < RW; i += 64u) img[i] = 0u;
   lds_u32 *pdw = (lds_u32 *)padb[wv];
@@ -512,12 +554,6 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   lds_u32 *rwm = (lds_u32 *)rawm[wv];
 #pragma unroll
   for (uint32_t i = 0; i < PDW / 64u; ++i) pdw[lane + 64u * i] = 0u;
-  const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
-  const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
-  const uint32_t t0 = blockIdx.x * WG + 64u * wv;
-  const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
-  const bool sl = lane < nstr;
-  const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
   // (thread s_me is lane `lane` of string t0 + lane)
   const uint32_t Eh_me = (bits_me + 7u) >> 3;  // Huffman bytes
   const uint32_t R_me = b_l - a_l;
@@ -530,23 +566,14 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
   uint4 wn = make_uint4(0, 0, 0, 0);  // the next round's chunk (prefetched)
   if (c0 + lane < c_end) wn = *reinterpret_cast<const uint4 *>(src + ((c0 + lane) << 4));
-  // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
-  // strings, L2-resident), summed with independent loads in flight, in 64
-  // bits (a batch's encoded total may pass the uint32 offset range)
-  uint64_t pre = 0;
-  if (tile_pre) {  // a large batch: the prefixes were scanned by k_tile_prefix64
-    // (pre is each thread's part of the sum the block scans add up)
-    pre = threadIdx.x == 0 ? tile_pre[blockIdx.x] : 0u;
-  } else {
-    uint64_t p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t t = threadIdx.x;
-    for (; t + 7u * WG < blockIdx.x; t += 8u * WG) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) p8[k] += tile_sums[t + k * WG];
+  if (vec) {
+    batch_sum(0u);
+    for (uint32_t base = 16u * WG; base < bt; base += 16u * WG) {  // (past 4096 tiles)
+      batch_load(base);
+      batch_sum(base);
     }
-    for (; t < blockIdx.x; t += WG) pre += tile_sums[t];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pre += p8[k];
+  } else if (!tile_pre) {
+    for (uint32_t t = threadIdx.x; t < bt; t += WG) pre += tile_sums[t];
   }
   uint32_t tot32, ptot_lo, ptot_hi;
   // the 64-bit prefix as two 32-bit sums: 256 parts of 23 bits fit 31 bits
@@ -554,7 +581,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
                                                &ptot_lo);  // (barriers)
   // (a string too long for the 32-bit code-bit counts poisoned the tile's
   // sum: the tile overflows)
-  const uint64_t tot = tile_sums[blockIdx.x] == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
+  const uint64_t tot = tsum == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
   {
     uint32_t dummy;
     block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
