@@ -350,10 +350,16 @@ size_t static_len(uint32_t idx, int which) {
 // hd_inflate_commit_indexed / newname / indname (:1780-1875), the table size
 // update rules (:1942-2003), add_hd_table_incremental, and the end-of-block
 // checks; the bad state is sticky (:1932-1934, :2276).
-void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls, BlockOut &out) {
-  out.recs.clear();
-  out.bytes.clear();
-  auto emit = [&](const char *n, size_t nl, const char *v, size_t vl, uint8_t flags) {
+// A block's fields go to a sink: its own buffers (BlockSink, placed in block
+// order after a parallel replay), or straight into the caller's arena and
+// field array (DirectSink: one connection, output bound within the caps).
+struct BlockSink {
+  BlockOut &out;
+  void begin() {
+    out.recs.clear();
+    out.bytes.clear();
+  }
+  void emit(const char *n, size_t nl, const char *v, size_t vl, uint8_t flags) {
     Rec r;
     r.flags = flags;
     r.name_off = (uint32_t)out.bytes.size();
@@ -365,6 +371,46 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
     out.bytes.append(v, vl);
     out.bytes.push_back('\0');
     out.recs.push_back(r);
+  }
+  // the field just emitted (the table copies it from here)
+  const uint8_t *last_name() const { return (const uint8_t *)out.bytes.data() + out.recs.back().name_off; }
+  const uint8_t *last_value() const { return (const uint8_t *)out.bytes.data() + out.recs.back().value_off; }
+  void finish(int32_t status) { out.status = status; }
+  int32_t count() const { return (int32_t)out.recs.size(); }
+};
+struct DirectSink {
+  uint8_t *arena;
+  nghttp2_amd_hd_nv *nva;
+  int32_t *status;
+  size_t ar = 0, nv = 0, nv0 = 0;
+  uint32_t block = 0;
+  void begin() { nv0 = nv; }
+  void emit(const char *n, size_t nl, const char *v, size_t vl, uint8_t flags) {
+    nghttp2_amd_hd_nv &d = nva[nv++];
+    d.block = block;
+    d.flags = flags;
+    d.name_off = (uint32_t)ar;
+    d.name_len = (uint32_t)nl;
+    if (nl) memcpy(arena + ar, n, nl);
+    arena[ar + nl] = 0;
+    ar += nl + 1;
+    d.value_off = (uint32_t)ar;
+    d.value_len = (uint32_t)vl;
+    if (vl) memcpy(arena + ar, v, vl);
+    arena[ar + vl] = 0;
+    ar += vl + 1;
+  }
+  const uint8_t *last_name() const { return arena + nva[nv - 1].name_off; }
+  const uint8_t *last_value() const { return arena + nva[nv - 1].value_off; }
+  void finish(int32_t st) { status[block] = st; }
+  int32_t count() const { return (int32_t)(nv - nv0); }
+};
+
+template <class Sink>
+void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls, Sink &out) {
+  out.begin();
+  auto emit = [&](const char *n, size_t nl, const char *v, size_t vl, uint8_t flags) {
+    out.emit(n, nl, v, vl, flags);
   };
   auto entry = [&](uint32_t idx, const char **n, size_t *nl, const char **v, size_t *vl) {
     if (idx < kStaticLen) {
@@ -431,11 +477,8 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
     }
     const uint8_t flags = op.no_index ? 1u : 0u;  // NGHTTP2_NV_FLAG_NO_INDEX
     emit(n, nl, v, vl, flags);
-    if (op.index_required) {  // the table copies the field just emitted
-      const Rec &r = out.recs.back();
-      const uint8_t *ob = (const uint8_t *)out.bytes.data();
-      inf->add(ob + r.name_off, nl, ob + r.value_off, vl);
-    }
+    if (op.index_required)  // the table copies the field just emitted
+      inf->add(out.last_name(), nl, out.last_value(), vl);
   }
   // truncated or malformed wire after the parsed representations; and a
   // block that ends while a table size update is still expected
@@ -443,9 +486,9 @@ void replay_block(nghttp2_amd_hd_inflater *inf, const Block &b, const LitSrc &ls
   if (ok && (!b.parse_ok || inf->expect_size)) ok = false;
   if (!ok) {
     inf->bad = true;
-    out.status = NGHTTP2_AMD_ERR_HEADER_COMP;  // the fields before the error stay emitted
+    out.finish(NGHTTP2_AMD_ERR_HEADER_COMP);  // the fields before the error stay emitted
   } else {
-    out.status = (int32_t)out.recs.size();
+    out.finish(out.count());
   }
 }
 
@@ -809,6 +852,55 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     }
   }
   ph.mark("bound");
+  if (conns.size() == 1) {
+    // one connection (a serial replay anyway): fields straight into the
+    // caller's arena and array in block order -- no per-block buffers, no
+    // placement pass (round 5: config 1's 1,000 blocks of one connection).
+    // A block whose own output bound may pass the caps is replayed into a
+    // scratch buffer from a copy of the table, and placed if it fits, else
+    // the table is restored and the batch cut there.
+    if (nh && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NGHTTP2_AMD_ERR_FATAL;
+    ph.mark("gpu wait");
+    nghttp2_amd_hd_inflater *c = conns[0];
+    DirectSink ds{arena, nva, block_status};
+    uint32_t cut = nblocks;
+    for (uint32_t i = 0; i < nblocks; ++i) {
+      const Block &b = bl[i];
+      const uint64_t rm = std::min<uint64_t>(std::max<size_t>({64u, c->settings_max, c->bufsize_max}), UINT32_MAX);
+      const uint64_t ar_b = b.ndyn && rm > (UINT64_MAX - b.ar) / b.ndyn ? UINT64_MAX : b.ar + b.ndyn * rm;
+      ds.block = i;
+      if (ds.nv + b.nv <= nva_cap && ar_b <= arena_cap - ds.ar) {
+        replay_block(c, b, ls, ds);
+        continue;
+      }
+      nghttp2_amd_hd_inflater keep = *c;
+      BlockOut scratch;
+      BlockSink bs{scratch};
+      replay_block(c, b, ls, bs);
+      if (ds.nv + scratch.recs.size() > nva_cap || scratch.bytes.size() > arena_cap - ds.ar) {
+        *c = std::move(keep);
+        cut = i;
+        break;
+      }
+      if (!scratch.bytes.empty()) memcpy(arena + ds.ar, scratch.bytes.data(), scratch.bytes.size());
+      for (const Rec &r : scratch.recs) {
+        nghttp2_amd_hd_nv &d = nva[ds.nv++];
+        d.block = i;
+        d.name_off = (uint32_t)ds.ar + r.name_off;
+        d.name_len = r.name_len;
+        d.value_off = (uint32_t)ds.ar + r.value_off;
+        d.value_len = r.value_len;
+        d.flags = r.flags;
+      }
+      ds.ar += scratch.bytes.size();
+      block_status[i] = scratch.status;
+    }
+    for (uint32_t j = cut; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
+    ph.mark("replay direct");
+    *nva_used = ds.nv;
+    *arena_used = ds.ar;
+    return cut < nblocks ? NGHTTP2_AMD_ERR_BUFFER_ERROR : 0;
+  }
   std::vector<nghttp2_amd_hd_inflater> snap;
   if (may_cut) {
     snap.reserve(conns.size());
@@ -821,7 +913,10 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   std::vector<BlockOut> &outs = E.outs;
   if (outs.size() < nblocks) outs.resize(nblocks);
   parallel_for(conns.size(), 1, [&](size_t c) {
-    for (uint32_t j = cstart[c]; j < cstart[c + 1]; ++j) replay_block(conns[c], bl[corder[j]], ls, outs[corder[j]]);
+    for (uint32_t j = cstart[c]; j < cstart[c + 1]; ++j) {
+      BlockSink bs{outs[corder[j]]};
+      replay_block(conns[c], bl[corder[j]], ls, bs);
+    }
   });
 
   ph.mark("replay");
@@ -849,7 +944,8 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   if (cut < nblocks) {  // restore, then re-apply the blocks before the cut
     for (size_t c = 0; c < conns.size(); ++c) *conns[c] = std::move(snap[c]);
     BlockOut scratch;
-    for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, scratch);
+    BlockSink ss{scratch};
+    for (uint32_t i = 0; i < cut; ++i) replay_block(inflaters[i], bl[i], ls, ss);
     for (uint32_t j = cut; j < nblocks; ++j) block_status[j] = NGHTTP2_AMD_ERR_BUFFER_ERROR;
   }
   parallel_for(cut, 256, [&](size_t i) {
