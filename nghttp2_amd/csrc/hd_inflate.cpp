@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -195,7 +196,7 @@ struct Op {
   uint32_t value = 0;  // SIZE: the new size; INDEXED / indexed-name LITERAL: the index
   Lit name{nullptr, 0, -1}, val{nullptr, 0, -1};
 };
-struct Block {
+struct alignas(128) Block {  // (aligned as BlockOut)
   std::vector<Op> ops;
   bool parse_ok = true;
   // the output bound's parts (pass 1): fields, bytes other than dynamic-table
@@ -208,9 +209,34 @@ struct Rec {
   uint32_t name_off, name_len, value_off, value_len;
   uint8_t flags;
 };
-struct BlockOut {
+// A growable byte buffer written through a raw pointer (no per-append
+// capacity check or zero fill): a block's name\0value\0 runs.
+struct ByteBuf {
+  std::unique_ptr<uint8_t[]> p;
+  size_t n = 0, cap = 0;
+  void clear() { n = 0; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const uint8_t *data() const { return p.get(); }
+  uint8_t *room(size_t k) {  // k more bytes at the end
+    if (n + k > cap) {
+      const size_t nc = std::max<size_t>(2 * cap, std::max<size_t>(n + k, 256));
+      std::unique_ptr<uint8_t[]> q(new uint8_t[nc]);
+      if (n) memcpy(q.get(), p.get(), n);
+      p.swap(q);
+      cap = nc;
+    }
+    uint8_t *r = p.get() + n;
+    n += k;
+    return r;
+  }
+};
+// (128-byte aligned: neighbouring blocks belong to different connections, so
+// different replay threads; on shared lines every emit's size update would
+// bounce the line between cores)
+struct alignas(128) BlockOut {
   std::vector<Rec> recs;
-  std::string bytes;
+  ByteBuf bytes;
   int32_t status = 0;
 };
 
@@ -364,12 +390,13 @@ struct BlockSink {
     r.flags = flags;
     r.name_off = (uint32_t)out.bytes.size();
     r.name_len = (uint32_t)nl;
-    out.bytes.append(n, nl);
-    out.bytes.push_back('\0');  // NUL-terminated like the reference's rcbufs (:2112, :2201)
-    r.value_off = (uint32_t)out.bytes.size();
+    r.value_off = r.name_off + (uint32_t)nl + 1u;
     r.value_len = (uint32_t)vl;
-    out.bytes.append(v, vl);
-    out.bytes.push_back('\0');
+    uint8_t *d = out.bytes.room(nl + vl + 2);
+    if (nl) memcpy(d, n, nl);
+    d[nl] = 0;  // NUL-terminated like the reference's rcbufs (:2112, :2201)
+    if (vl) memcpy(d + nl + 1, v, vl);
+    d[nl + 1 + vl] = 0;
     out.recs.push_back(r);
   }
   // the field just emitted (the table copies it from here)
