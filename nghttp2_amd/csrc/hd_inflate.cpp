@@ -280,6 +280,8 @@ bool grow_host(void **p, size_t *cap, size_t need) {
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
+  // (coherent: a non-coherent mapping measured the same, round 5,
+  // profiles/r05/inflate/pin_modes.log)
   if (!hip_ok(hipHostMalloc(p, need, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc")) return false;
   *cap = need;
   return true;
@@ -703,6 +705,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     bl[i].ar = ar;
     bl[i].ndyn = nd;
   });
+  ph.mark("parse blocks");
   for (uint32_t i = 0; i < nblocks; ++i) {
     nhuff[i + 1] += nhuff[i];
     E.hbytes[i + 1] += E.hbytes[i];
@@ -744,6 +747,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
                        !grow_dev((void **)&E.d_off, &E.dn_cap, meta)))
       return NGHTTP2_AMD_ERR_NOMEM;
   }
+  ph.mark("pools");
   hoff[0] = 0;
   uint8_t *const hp = E.h_pool;
   parallel_for(nblocks, 64, [&](size_t i) {  // each block numbers and places its literals
@@ -766,7 +770,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     }
   });
 
-  ph.mark("parse");
+  ph.mark("number+copy");
   const uint8_t *dec = nullptr;
   const uint32_t *slot = nullptr;
   const int32_t *hst = nullptr;
