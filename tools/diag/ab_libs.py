@@ -106,7 +106,11 @@ for cfg in [int(c) for c in sys.argv[1:]] or [3, 2, 5]:
         ecap = codec.encode_bound(int(off[-1]), n)
         edst = torch.empty(ecap, dtype=torch.uint8, device=dev)
         eoff = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        wsz = codec.L.nghttp2_amd_hd_huff_encode_workspace_size(int(off[-1]), n)
+        # (the largest workspace any library asks for: their layouts may differ)
+        for L_ in libs.values():
+            L_.nghttp2_amd_hd_huff_encode_workspace_size.restype = sz
+            L_.nghttp2_amd_hd_huff_encode_workspace_size.argtypes = [u64, u32]
+        wsz = max(L_.nghttp2_amd_hd_huff_encode_workspace_size(int(off[-1]), n) for L_ in libs.values())
         ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
 
         def encf(k):
