@@ -1401,6 +1401,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #endif
 #ifndef DD_TAILU
 #define DD_TAILU 2u  // the workgroup's last DD_TAILU x waves units are claimed singly
+#ifndef DD_JIT_TAIL
+#define DD_JIT_TAIL 1  // a tail unit is claimed when the wave's task ends, not one task ahead
+#endif
 #endif
 #ifndef DD_SK40
 #define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)
@@ -1916,12 +1919,19 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
                                                   : t_lo)
                                  : t_hi;
   uint32_t next_k = 0;
-  auto claim_next = [&](uint32_t) -> uint32_t {
+  // (defer, DD_JIT_TAIL: a claim that finds the range's whole tasks gone
+  // returns kDefer and the wave claims its tail unit when its task ends:
+  // claimed one task ahead, the tail units were all handed out a task before
+  // the workgroup's end, by stale order, and its waves ended ~22 us apart)
+  constexpr uint32_t kDefer = 0xFFFFFFFFu;
+  auto claim_next = [&](bool defer, bool tail_only = false) -> uint32_t {
     uint32_t t = 0;
     if (lane == 0) {
-      const uint32_t v = atomicAdd((uint32_t *)&S.claimed, 1u);
-      t = t_lo + TK * v;
-      if (TK > 1u && t + TK > t_mid) {
+      const uint32_t v = tail_only ? 0u : atomicAdd((uint32_t *)&S.claimed, 1u);
+      t = tail_only ? t_mid : t_lo + TK * v;
+      if (TK > 1u && t + TK > t_mid && defer) {
+        t = kDefer;
+      } else if (TK > 1u && t + TK > t_mid) {
         const uint32_t c = atomicAdd((uint32_t *)&S.claimed1, 1u);
         if (kBal && c < t_hi - t_mid) {
           while (__hip_atomic_load((uint32_t *)&S.tready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
@@ -1937,6 +1947,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     next_k = t < t_hi ? (t < t_mid ? TK : 1u) : 0u;
     return t;
   };
+  constexpr bool kJit = TK > 1u && DD_JIT_TAIL != 0;
   // a task's string offsets are loaded one task ahead, and the first round
   // of the next task is staged into registers during the current task's
   // last round (pf), so neither waits at a task start
@@ -1957,7 +1968,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   };
   uint4 pf[kPF];
   uint32_t pf_IB = 0xFFFFFFFFu;
-  const uint32_t t_first = claim_next(0u);
+  const uint32_t t_first = claim_next(false);
   uint32_t task_k = next_k;
   load_offs(t_first < t_hi ? t_first : ntask, task_k, na_l, nb_l);
   uint32_t next_task = t_hi;
@@ -1968,7 +1979,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   bool dmode = false;
   uint32_t nslow = 0;
   for (uint32_t task = t_first; task < t_hi;) {
-    next_task = claim_next(task);
+    next_task = claim_next(kJit);
     const uint32_t t0 = task * TS;
     const uint32_t nstr = min(n - t0, TS * task_k);
     const bool sl = lane < nstr;
@@ -2252,6 +2263,10 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kJit && next_task == kDefer) {
+      next_task = claim_next(false, true);
+      load_offs(next_task < t_hi ? next_task : ntask, next_k, na_l, nb_l);
+    }
     task = next_task;
     task_k = next_k;
   }
