@@ -1401,9 +1401,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #endif
 #ifndef DD_TAILU
 #define DD_TAILU 2u  // the workgroup's last DD_TAILU x waves units are claimed singly
+#endif
 #ifndef DD_JIT_TAIL
 #define DD_JIT_TAIL 1  // a tail unit is claimed when the wave's task ends, not one task ahead
-#endif
 #endif
 #ifndef DD_SK40
 #define DD_SK40 2u  // the 40-byte instance serves long codes every 2nd pair (dd_run SLOWK)

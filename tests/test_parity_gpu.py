@@ -649,3 +649,33 @@ def test_decode_instance_batch_sizes(codec, dev, n, pick):
     pool, off = W.gen_mixed_values(n, seed=1000 + n)
     enc, eoff = O.encode_batch(pool, off, nthreads=8)
     auto_decode_check(codec, dev, enc, eoff, "%s n=%d" % (pick, n), pick=pick, nthreads=8)
+
+
+def test_decode_auto_concurrent_streams(codec, dev):
+    """The 40-byte instance's cross-workgroup tail stealing (DD_STEAL) with
+    launches that run at the same time and share the steal records: three
+    streams each decode their own batch of long values four times, launched
+    back to back; every string's status and bytes equal its raw input (a lost
+    tail unit would leave its strings' status and bytes unwritten)."""
+    import torch
+    from nghttp2_amd import workloads as W
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    batches = []
+    for k in range(3):
+        pool, off = W.gen_mixed_values(60000 + 7000 * k, seed=7700 + k)
+        enc, eoff = gpu_encode(codec, dev, pool, off)
+        batches.append((pool, off, to_dev(pad16(enc, eoff[-1]), dev), to_dev(eoff, dev), int(eoff[-1])))
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(4):
+        for s, (pool, off, src, so, eb) in zip(streams, batches):
+            s.wait_stream(torch.cuda.current_stream())
+            outs.append((rep, pool, off) + tuple(codec.decode_auto(src, so, enc_bytes=eb, stream=s)))
+    torch.cuda.synchronize()
+    for rep, pool, off, dst, do, st in outs:
+        raw = np.diff(off.astype(np.int64))
+        assert np.array_equal(st.cpu().numpy(), raw), rep
+        d = dst.cpu().numpy()
+        do = do.cpu().numpy().view(np.uint32).astype(np.int64)
+        rel = np.arange(int(raw.sum())) - np.repeat(np.cumsum(raw) - raw, raw)
+        assert np.array_equal(d[np.repeat(do[:-1], raw) + rel], pool[:int(off[-1])]), rep
