@@ -540,8 +540,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
              (uint64_t)(i + 2u < bt ? v[k].z : 0u) + (i + 3u < bt ? v[k].w : 0u);
     }
   };
-  if (tile_pre) {  // a large batch: the prefixes were scanned by k_tile_prefix64
-    pre = threadIdx.x == 0 ? tile_pre[bt] : 0u;
+  if (tile_pre) {  // the prefixes were scanned by k_tile_prefix64 (every thread reads its tile's)
+    pre = tile_pre[bt];
   } else if (vec) {
     batch_load(0u);
   }
@@ -575,18 +575,19 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   } else if (!tile_pre) {
     for (uint32_t t = threadIdx.x; t < bt; t += WG) pre += tile_sums[t];
   }
-  uint32_t tot32, ptot_lo, ptot_hi;
+  uint32_t tot32, ptot_lo, ptot_hi = 0;
   // the 64-bit prefix as two 32-bit sums: 256 parts of 23 bits fit 31 bits
-  const uint32_t loc = block_excl_scan_sum<WG>(E_me, (uint32_t)(pre & 0x7FFFFFu), red, &tot32,
+  // (tile_pre: every thread holds the whole prefix, no sum)
+  const uint32_t loc = block_excl_scan_sum<WG>(E_me, tile_pre ? 0u : (uint32_t)(pre & 0x7FFFFFu), red, &tot32,
                                                &ptot_lo);  // (barriers)
   // (a string too long for the 32-bit code-bit counts poisoned the tile's
   // sum: the tile overflows)
   const uint64_t tot = tsum == 0xFFFFFFFFu ? 0x100000000ull : (uint64_t)tot32;
-  {
+  if (!tile_pre) {
     uint32_t dummy;
     block_excl_scan_sum<WG>(0u, (uint32_t)(pre >> 23), red, &dummy, &ptot_hi);
   }
-  const uint64_t ptot = ((uint64_t)ptot_hi << 23) + ptot_lo;
+  const uint64_t ptot = tile_pre ? pre : ((uint64_t)ptot_hi << 23) + ptot_lo;
   // uint32 offsets: a tile whose strings would end past the limit writes no
   // bytes, saturated offsets and the overflow mark in dst_off[n]
   const uint64_t limit = dst_cap < 0xFFFFFFFEull ? dst_cap : 0xFFFFFFFEull;
