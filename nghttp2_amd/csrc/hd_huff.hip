@@ -15,7 +15,9 @@
 //                   95-101) counted as length of its last byte, codes combined
 //                   into pairs and quads in registers and OR'ed into an LDS
 //                   image that leaves as whole big-endian dwords
-//   k_decode_items  decode_batch_auto: persistent waves, tasks of 64 strings,
+//   k_decode_items  decode_batch_auto: persistent waves, tasks of 64 strings
+//                   (a workgroup range's last ones as 32-string units,
+//                   claimed largest first when a wave frees up),
 //                   rounds of up to 64 items (a whole string, or a 40-byte
 //                   piece of a long one, warmed up and verified; the
 //                   64-byte instance cuts a round at an input-byte budget);
