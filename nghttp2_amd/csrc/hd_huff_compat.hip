@@ -8,11 +8,13 @@
 //
 // Threading follows nghttp2's model (doc/programmers-guide.rst:35-40: one
 // session per thread, nothing shared): every calling host thread gets its
-// own engine -- HIP stream, device buffer, pinned staging -- on the device
-// current in that thread at its first call, so concurrent callers never
-// serialise on a lock or a stream.  A call is one round trip: one H2D of
-// the string and its metadata from one pinned block, the kernels, one D2H
-// of the results and output bytes into it, one synchronisation.
+// own engine -- HIP stream, a mapped pinned block, device workspace -- on the
+// device current in that thread at its first call, so concurrent callers
+// never serialise on a lock or a stream.  A call is one round trip without
+// copies: the kernels read the string and its metadata from the mapped
+// block and write the results and output bytes into it (round 5: an H2D and
+// a D2H copy around the kernels took 21.0 / 26.7 us per encode pair /
+// decode), then one synchronisation.
 //
 // emit_string (lib/nghttp2_hd.c:1009, :1037) asks for the count and then,
 // when Huffman wins, for the encoding of the same bytes.  The count runs the
@@ -61,7 +63,7 @@ struct Engine {
   bool ready = false;
   int device = -1;
   hipStream_t st = nullptr;
-  uint8_t *d_buf = nullptr, *h_pin = nullptr;
+  uint8_t *d_buf = nullptr, *h_pin = nullptr;  // d_buf: h_pin's device address
   size_t cap = 0;
   void *d_ws = nullptr;
   size_t ws = 0;
@@ -71,7 +73,6 @@ struct Engine {
 
   ~Engine() { release(); }
   void release() {
-    if (d_buf) (void)hipFree(d_buf);
     if (h_pin) (void)hipHostFree(h_pin);
     if (d_ws) (void)hipFree(d_ws);
     if (st) (void)hipStreamDestroy(st);
@@ -107,14 +108,17 @@ struct Engine {
     }
     if (need > cap) {
       need = round16(need) + 4096;
-      if (d_buf) (void)hipFree(d_buf);
       if (h_pin) (void)hipHostFree(h_pin);
       d_buf = nullptr;
       h_pin = nullptr;
       cap = 0;
-      if (!hip_ok(hipMalloc(&d_buf, need)) ||
-          !hip_ok(hipHostMalloc((void **)&h_pin, need, hipHostMallocDefault)))
+      if (!hip_ok(hipHostMalloc((void **)&h_pin, need, hipHostMallocMapped | hipHostMallocCoherent)))
         return false;
+      if (!hip_ok(hipHostGetDevicePointer((void **)&d_buf, h_pin, 0))) {
+        (void)hipHostFree(h_pin);
+        h_pin = nullptr;
+        return false;
+      }
       cap = need;
     }
     return true;
@@ -126,11 +130,10 @@ Engine &eng() {
   return e;
 }
 
-// H2D of the string (zero padded) and the first `meta_bytes` of meta
-bool upload(Engine &e, const Layout &l, const uint8_t *src, size_t len, size_t meta_bytes) {
+// the string (zero padded) into the mapped block, ahead of its metadata
+void upload(Engine &e, const Layout &l, const uint8_t *src, size_t len) {
   if (len) memcpy(e.h_pin, src, len);
   memset(e.h_pin + len, 0, l.meta - len);
-  return hip_ok(hipMemcpyAsync(e.d_buf, e.h_pin, l.meta + meta_bytes, hipMemcpyHostToDevice, e.st));
 }
 
 // the whole encode of one string: the kept output on success
@@ -142,12 +145,11 @@ bool encode_one(Engine &e, const uint8_t *src, size_t len) {
   uint32_t *m = reinterpret_cast<uint32_t *>(e.h_pin + l.meta);
   m[0] = 0;
   m[1] = (uint32_t)len;
-  if (!upload(e, l, src, len, 8)) return false;
+  upload(e, l, src, len);
   uint8_t *d = e.d_buf;
   if (nghttp2_amd_hd_huff_encode_batch(d, reinterpret_cast<const uint32_t *>(d + l.meta), 1, d + l.out,
                                        e.cap - l.out, reinterpret_cast<uint32_t *>(d + l.res), e.d_ws,
                                        e.ws, e.st) != 0 ||
-      !hip_ok(hipMemcpyAsync(e.h_pin + l.res, d + l.res, 16 + bound, hipMemcpyDeviceToHost, e.st)) ||
       !hip_ok(hipStreamSynchronize(e.st)))
     return false;
   const uint32_t *r = reinterpret_cast<const uint32_t *>(e.h_pin + l.res);
@@ -222,14 +224,13 @@ nghttp2_ssize nghttp2_hd_huff_decode(nghttp2_hd_huff_decode_context *ctx, nghttp
   memcpy(m, offs, sizeof offs);
   memcpy(m + 16, &ctx->fstate, 2);
   m[18] = ctx->flags;
-  if (!upload(e, l, src, srclen, 20)) return NGHTTP2_AMD_ERR_NOMEM;
+  upload(e, l, src, srclen);
   uint8_t *d = e.d_buf;
   const uint32_t *dm = reinterpret_cast<const uint32_t *>(d + l.meta);
   if (nghttp2_amd_hd_huff_decode_fsm_batch(d, dm, 1, d + l.out, dm + 2, reinterpret_cast<int32_t *>(d + l.res),
                                            reinterpret_cast<uint16_t *>(d + l.res + 4), d + l.res + 6,
                                            reinterpret_cast<const uint16_t *>(d + l.meta + 16),
                                            d + l.meta + 18, 0, e.st) != 0 ||
-      !hip_ok(hipMemcpyAsync(e.h_pin + l.res, d + l.res, 16 + cap, hipMemcpyDeviceToHost, e.st)) ||
       !hip_ok(hipStreamSynchronize(e.st)))
     return NGHTTP2_AMD_ERR_NOMEM;
   int32_t st;
