@@ -651,12 +651,30 @@ def test_decode_instance_batch_sizes(codec, dev, n, pick):
     auto_decode_check(codec, dev, enc, eoff, "%s n=%d" % (pick, n), pick=pick, nthreads=8)
 
 
+@pytest.mark.parametrize("where", ["tail", "head"])
+def test_decode_pieces40_skewed_lengths(codec, dev, where):
+    """Just-in-time tail claims with the work skewed: 60,000 short values and
+    2,000 of 1-4 KB placed at the batch's end (every workgroup range's tail
+    units are the heavy ones) or its start -- status, state and bytes per
+    string against the oracle."""
+    rng = np.random.default_rng(4242)
+    short = rng.integers(16, 41, size=60000)
+    long_ = rng.integers(1000, 4097, size=2000)
+    lengths = np.concatenate([short, long_] if where == "tail" else [long_, short]).astype(np.int64)
+    off = np.zeros(len(lengths) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum(lengths)
+    pool = rng.integers(32, 127, size=int(off[-1]), dtype=np.uint8)
+    enc, eoff = O.encode_batch(pool, off, nthreads=8)
+    auto_decode_check(codec, dev, enc, eoff, "skewed %s" % where, pick="pieces40", nthreads=8)
+
+
 def test_decode_auto_concurrent_streams(codec, dev):
-    """The 40-byte instance's cross-workgroup tail stealing (DD_STEAL) with
-    launches that run at the same time and share the steal records: three
-    streams each decode their own batch of long values four times, launched
-    back to back; every string's status and bytes equal its raw input (a lost
-    tail unit would leave its strings' status and bytes unwritten)."""
+    """The 40-byte instance's just-in-time tail claims with launches that run
+    at the same time (round 5 also measured, and dropped, cross-workgroup
+    stealing whose records such launches share): three streams each decode
+    their own batch of long values four times, launched back to back; every
+    string's status and bytes equal its raw input (a lost tail unit would
+    leave its strings' status and bytes unwritten)."""
     import torch
     from nghttp2_amd import workloads as W
     streams = [torch.cuda.Stream(dev) for _ in range(3)]
