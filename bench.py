@@ -48,6 +48,7 @@ CONFIG_NAMES = {
     5: "decode-only adversarial batch (1M strings: 30-bit codes, EOS, padding cases), 1xMI355X",
 }
 CPU_SAMPLE = 1 << 20  # strings of the cpu_baseline sample (bounded CPU work)
+BATCH_SEED_STEP = 104729  # seed offset of rotated batch b (--batches)
 
 
 def parse():
@@ -62,6 +63,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="config 3: skip the config-2 secondary measurement")
+    ap.add_argument("--batches", type=int, default=3,
+                    help="configs 2/3: distinct input batches rotated over the steps (step i "
+                         "encodes batch i %% B), so no step re-reads the raw input the step "
+                         "before it left in the caches; config 4 keeps one fixed set")
+    ap.add_argument("--secondary-ms", type=float, default=30.0,
+                    help="config 2 secondary: at least this long a timed window")
     ap.add_argument("--streams", type=int, default=2,
                     help="pipeline the steps over this many streams (step i on stream i %% S)")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -96,19 +103,39 @@ def cpu_info():
     if omp and omp.isdigit() and int(omp) > 0:
         usable = min(aff, int(omp))
     return {"nproc": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
-            "cpu_model": model, "usable": usable}
+            "cpu_model": model, "usable": usable, "cgroup_cpu_limit": cgroup_cpu_limit()}
 
 
-def cpu_baseline_roundtrip(pool, off, threads):
+def cgroup_cpu_limit():
+    """The CPU bandwidth this job's cgroup allows, in CPUs (cgroup v2
+    cpu.max, or v1 cfs quota / period), or None when unlimited or unreadable:
+    the evidence for the thread count of the cpu_baseline leg."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_roundtrip(pool, off, threads, extra=()):
     """Oracle (port of lib/nghttp2_hd_huffman.c) timed on host cores:
     count+encode then decode(final=1), best of repeats; same B accounting."""
     from oracle import oracle as O
     n = len(off) - 1
     raw = int(off[-1])
     res = {}
-    for nth in sorted({1, threads}):
+    for nth in sorted({1, threads} | set(extra)):
         best = None
-        reps = 3 if nth == 1 else 5
+        reps = 3 if nth == 1 or nth in extra else 5
         for _ in range(reps + 1):  # first rep is the warm-up
             te, td, etot, st = O.roundtrip_timed(pool, off, nth)
             assert (st >= 0).all()
@@ -196,17 +223,19 @@ def main():
         dist.all_reduce(t, op=op)
         return float(t.item())
 
-    def gen(c, rank_):
-        """(pool, off, scaling, seed text) of configuration c for this rank."""
-        seed = W.SEED[c] + 7919 * rank_  # each rank its own batch (weak scaling)
+    def gen(c, rank_, b=0):
+        """(pool, off, scaling, seed text) of configuration c for this rank
+        (b: the rotated batch's index; batch 0 is the one earlier rounds used)."""
+        seed = W.SEED[c] + 7919 * rank_ + BATCH_SEED_STEP * b  # each rank its own batch (weak scaling)
+        seed_txt = "numpy PCG64, seed 0x%X + 7919*rank + %d*batch" % (W.SEED[c], BATCH_SEED_STEP)
         if c == 2:
             n = args.strings or (1 << 20)
             pool, off = W.gen_pseudo_headers(n, seed=seed)
-            return pool, off, "weak", "numpy PCG64, seed 0x%X + 7919*rank" % W.SEED[c]
+            return pool, off, "weak", seed_txt
         if c == 3:
             n = args.strings or (1 << 20)
             pool, off = W.gen_mixed_values(n, seed=seed)
-            return pool, off, "weak", "numpy PCG64, seed 0x%X + 7919*rank" % W.SEED[c]
+            return pool, off, "weak", seed_txt
         # config 4: one fixed set, byte-balanced contiguous shard per rank
         from nghttp2_amd import shard as S
         n_total = args.strings or (1 << 24)
@@ -222,16 +251,21 @@ def main():
     if cfg == 5:
         out = run_decode_only(args, torch, dist, nghttp2_amd, W, dev, world, rank, allreduce)
     else:
-        pool, off, scaling, data = gen(cfg, rank)
-        progress("generated %d strings, %d bytes" % (len(off) - 1, int(off[-1])))
+        nb = 1 if cfg == 4 else max(1, args.batches)
+        batches = [gen(cfg, rank, b) for b in range(nb)]
+        pool, off, scaling, data = batches[0]
+        progress("generated %d batch(es) of %d strings, %d bytes (batch 0)"
+                 % (nb, len(off) - 1, int(off[-1])))
         out, ctx = run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce,
-                                 pool, off, cfg, scaling, data)
+                                 [(b[0], b[1]) for b in batches], cfg, scaling, data)
         if cfg == 3 and not args.no_secondary:
-            p2, o2, _, _ = gen(2, rank)
+            b2 = [gen(2, rank, b)[:2] for b in range(nb)]
             sec, _ = run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce,
-                                   p2, o2, 2, "weak", "", host_resident=False)
-            out["secondary"] = {"config2": {k: sec[k] for k in ("value", "ms_per_step")}}
+                                   b2, 2, "weak", "", host_resident=False,
+                                   min_window_ms=args.secondary_ms)
+            out["secondary"] = {"config2": {k: sec[k] for k in ("value", "ms_per_step", "steps")}}
             out["secondary"]["config2"].update(
+                timed_ms=round(sec["ms_per_step"] * sec["steps"], 2),
                 workload=CONFIG_NAMES[2], strings_per_gpu=sec["config"]["strings_per_gpu"],
                 raw_bytes_per_gpu=sec["config"]["raw_bytes_per_gpu"], roofline=sec["roofline"])
         if rank == 0 and not args.no_cpu_baseline and world == 1:
@@ -240,18 +274,25 @@ def main():
             threads = args.cpu_threads or info["usable"]
             ns = min(len(off) - 1, CPU_SAMPLE)
             sp, so = pool, off[:ns + 1]
-            res = cpu_baseline_roundtrip(sp, so, threads)
+            # also as many threads as the affinity mask holds (the whole
+            # machine's CPUs on the GPU box), beside the job's share
+            aff = info["affinity"]
+            res = cpu_baseline_roundtrip(sp, so, threads, extra=(aff,) if aff != threads else ())
             out["cpu_baseline"] = {
                 "value": round(res[threads][0], 4), "unit": "GB/s", "cores": threads,
                 "kind": "port",
+                "kind_note": "the oracle's C restatement: the reference's lib/nghttp2_hd_huffman.c "
+                             "does not compile on its own here (nghttp2.h includes the generated "
+                             "nghttp2ver.h), so it is not timed itself",
                 "sample": "%d strings (%s) of this workload, oracle/huff_oracle.c (C restatement "
                           "of lib/nghttp2_hd_huffman.c, gcc -O2), count+encode+decode(final=1), "
                           "best of 5 after 1 warm-up, %d pthreads; 1 thread: %.4f GB/s"
                           % (ns, "the whole batch" if ns == len(off) - 1 else "the first",
                              threads, res[1][0]),
                 "value_1thread": round(res[1][0], 4),
+                "value_affinity_threads": round(res[aff][0], 4), "affinity_threads": aff,
                 "host": {k: info[k] for k in ("cpu_model", "nproc", "affinity",
-                                              "omp_num_threads")}}
+                                              "omp_num_threads", "cgroup_cpu_limit")}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -266,26 +307,36 @@ def main():
 EVENT_STEPS_MIN = 100
 
 
-def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, off, cfg,
-                  scaling, data, host_resident=None):
-    n = len(off) - 1
-    raw_bytes = int(off[-1])
-    src = torch.from_numpy(pool).to(dev)
-    src_off = torch.from_numpy(off.view(np.int32)).to(dev)
+def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, batches, cfg,
+                  scaling, data, host_resident=None, min_window_ms=0.0):
+    """batches: [(pool, off)] rotated over the steps (step i encodes batch
+    i % len(batches)); min_window_ms > 0 (the secondary): time more than
+    --steps steps if that is needed for a timed window at least that long."""
+    nb = len(batches)
+    srcs, srcs_off, raws, ns, enc_totals = [], [], [], [], []
     codec0 = nghttp2_amd.HuffmanBatchCodec(dev)
-    # the encoded size, once, to size every pipe's decode pool from the
-    # actual E (not the 30-bit worst case)
-    enc_cap = codec0.encode_bound(raw_bytes, n)
-    probe_enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
-    probe_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    progress("config %d: inputs on the device" % cfg)
-    codec0.encode(src, src_off, raw_bytes=raw_bytes, dst=probe_enc, dst_off=probe_off)
-    enc_total = int(probe_off[-1].item()) & 0xFFFFFFFF
-    progress("config %d: encoded %d bytes" % (cfg, enc_total))
-    assert enc_total != 0xFFFFFFFF, "encoded total overflows the uint32 offsets"
-    del probe_enc, probe_off
-    enc_cap = min(enc_cap, enc_total + 4096)  # the kernels never write past dst_cap
-    dec_cap = codec0.decode_bound(enc_total, n)
+    for pool_b, off_b in batches:
+        n_b, raw_b = len(off_b) - 1, int(off_b[-1])
+        srcs.append(torch.from_numpy(pool_b).to(dev))
+        srcs_off.append(torch.from_numpy(off_b.view(np.int32)).to(dev))
+        # the encoded size, once, to size every pipe's decode pool from the
+        # actual E (not the 30-bit worst case)
+        cap_b = codec0.encode_bound(raw_b, n_b)
+        probe_enc = torch.empty(cap_b, dtype=torch.uint8, device=dev)
+        probe_off = torch.empty(n_b + 1, dtype=torch.int32, device=dev)
+        codec0.encode(srcs[-1], srcs_off[-1], raw_bytes=raw_b, dst=probe_enc, dst_off=probe_off)
+        e_b = int(probe_off[-1].item()) & 0xFFFFFFFF
+        assert e_b != 0xFFFFFFFF, "encoded total overflows the uint32 offsets"
+        del probe_enc, probe_off
+        raws.append(raw_b)
+        ns.append(n_b)
+        enc_totals.append(e_b)
+    progress("config %d: %d batch(es) on the device, encoded %s bytes" % (cfg, nb, enc_totals))
+    pool, off = batches[0]
+    n, raw_bytes, enc_total = ns[0], raws[0], enc_totals[0]
+    n_max = max(ns)
+    enc_cap = max(e + 4096 for e in enc_totals)  # the kernels never write past dst_cap
+    dec_cap = max(codec0.decode_bound(e, k) for e, k in zip(enc_totals, ns))
 
     class Pipe:
         """One stream with its own output buffers and workspace: --streams S
@@ -297,22 +348,25 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
             self.codec = nghttp2_amd.HuffmanBatchCodec(dev)
             self.stream = stream
             self.enc = torch.empty(enc_cap, dtype=torch.uint8, device=dev)
-            self.enc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            self.dec_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            self.enc_off = torch.empty(n_max + 1, dtype=torch.int32, device=dev)
+            self.dec_off = torch.empty(n_max + 1, dtype=torch.int32, device=dev)
             self.dec = torch.empty(dec_cap, dtype=torch.uint8, device=dev)
-            self.status = torch.empty(n, dtype=torch.int32, device=dev)
-            self.src, self.src_off = src, src_off  # --host-resident: the pipe's own copies
+            self.status = torch.empty(n_max, dtype=torch.int32, device=dev)
+            self.host_src = None  # --host-resident: the pipe's own copies of batch 0
 
-        def run(self, evs=None):
+        def run(self, b, evs=None):
             st = self.stream
+            k = ns[b]
+            src_b, off_b = (srcs[b], srcs_off[b]) if self.host_src is None else self.host_src
             if evs is not None:
                 evs[0].record(st)
-            self.codec.encode(self.src, self.src_off, raw_bytes=raw_bytes, dst=self.enc,
-                              dst_off=self.enc_off, stream=st)
+            self.codec.encode(src_b, off_b, raw_bytes=raws[b], dst=self.enc,
+                              dst_off=self.enc_off[:k + 1], stream=st)
             if evs is not None:
                 evs[1].record(st)
-            self.codec.decode_auto(self.enc, self.enc_off, enc_bytes=enc_total, dst=self.dec,
-                                   dst_off=self.dec_off, status=self.status, stream=st)
+            self.codec.decode_auto(self.enc, self.enc_off[:k + 1], enc_bytes=enc_totals[b],
+                                   dst=self.dec, dst_off=self.dec_off[:k + 1],
+                                   status=self.status[:k], stream=st)
             if evs is not None:
                 evs[2].record(st)
 
@@ -324,47 +378,63 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
            torch.cuda.Event(enable_timing=True)) for _ in range(KE)]
 
     for w in range(args.warmup):
-        for p in pipes:
-            p.run()
+        for k, p in enumerate(pipes):
+            p.run((w * len(pipes) + k) % nb)
         torch.cuda.synchronize()
         progress("config %d: warm-up step %d" % (cfg, w))
-    for p in pipes[1:]:  # every pipe decodes the batch exactly
-        assert torch.equal(p.status, P0.status) and torch.equal(p.enc_off, P0.enc_off)
 
-    progress("config %d: warm-up done, checking the round trip" % cfg)
-    # correctness gate on this rank's batch (fails loudly, never measured)
-    st = P0.status.cpu().numpy()
+    progress("config %d: warm-up done, checking the round trips" % cfg)
+    # correctness gate on every batch of this rank (fails loudly, never
+    # measured); batch 0 last, so P0 holds it for --dump-dir
+    for b in reversed(range(nb)):
+        for p in pipes:
+            p.run(b)
+        torch.cuda.synchronize()
+        k = ns[b]
+        for p in pipes[1:]:  # every pipe decodes the batch exactly
+            assert torch.equal(p.status[:k], P0.status[:k])
+            assert torch.equal(p.enc_off[:k + 1], P0.enc_off[:k + 1])
+        st_b = P0.status[:k].cpu().numpy()
+        assert np.array_equal(st_b, np.diff(batches[b][1].astype(np.int64))), \
+            "decode(encode(x)) length mismatch"
+        assert int(P0.enc_off[k].item()) & 0xFFFFFFFF == enc_totals[b]
+        verify_roundtrip(P0.dec, P0.dec_off[:k + 1].cpu().numpy().view(np.uint32), *batches[b])
+    st = P0.status[:n].cpu().numpy()
     raw_len = np.diff(off.astype(np.int64))
-    assert np.array_equal(st, raw_len), "decode(encode(x)) length mismatch"
-    assert int(P0.enc_off[-1].item()) & 0xFFFFFFFF == enc_total
-    verify_roundtrip(P0.dec, P0.dec_off.cpu().numpy().view(np.uint32), pool, off)
     if args.dump_dir:
         rk = int(os.environ.get("RANK", "0"))
         np.savez(os.path.join(args.dump_dir, "rank%d.npz" % rk), data=np.array(data),
                  enc=P0.enc[:enc_total].cpu().numpy(),
-                 enc_off=P0.enc_off.cpu().numpy().view(np.uint32), status=st,
-                 dec=P0.dec[:int(P0.dec_off[-1].item()) & 0xFFFFFFFF].cpu().numpy(),
-                 dec_off=P0.dec_off.cpu().numpy().view(np.uint32))
+                 enc_off=P0.enc_off[:n + 1].cpu().numpy().view(np.uint32), status=st,
+                 dec=P0.dec[:int(P0.dec_off[n].item()) & 0xFFFFFFFF].cpu().numpy(),
+                 dec_off=P0.dec_off[:n + 1].cpu().numpy().view(np.uint32))
 
-    progress("config %d: round trip checked, timing" % cfg)
+    progress("config %d: round trips checked, timing" % cfg)
     # per-kernel timing (roofline): K plain steps with events on the stream
     for i in range(KE):
-        P0.run(ev[i])
+        P0.run(i % nb, ev[i])
     torch.cuda.synchronize()
+    t_enc = np.mean([ev[i][0].elapsed_time(ev[i][1]) for i in range(KE)]) * 1e-3
+    t_dec = np.mean([ev[i][1].elapsed_time(ev[i][2]) for i in range(KE)]) * 1e-3
+
+    steps = args.steps
+    if min_window_ms > 0:  # (the two-stream step is shorter than enc + dec)
+        steps = max(steps, int(np.ceil(min_window_ms / (0.7 * (t_enc + t_dec) * 1e3))))
 
     # the timed steps: plain launches on the streams (no events in between)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        pipes[i % len(pipes)].run()
+    for i in range(steps):
+        pipes[i % len(pipes)].run(i % nb)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    B_rank = 2 * raw_bytes + 2 * enc_total + 24 * n
+    B_b = [2 * r + 2 * e + 24 * k for r, e, k in zip(raws, enc_totals, ns)]
+    B_rank = sum(B_b[i % nb] for i in range(steps))  # all the timed steps
     if world > 1:
         import torch.distributed as dist_
         elapsed = allreduce(elapsed, dist_.ReduceOp.MAX)
@@ -372,18 +442,18 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
     else:
         B_total = float(B_rank)
 
-    t_enc = np.mean([ev[i][0].elapsed_time(ev[i][1]) for i in range(KE)]) * 1e-3
-    t_dec = np.mean([ev[i][1].elapsed_time(ev[i][2]) for i in range(KE)]) * 1e-3
-    ms_per_step = elapsed / args.steps * 1e3
-    value = B_total * args.steps / elapsed / 1e9
+    ms_per_step = elapsed / steps * 1e3
+    value = B_total / elapsed / 1e9
 
     # roofline of the dominant kernel: k_decode_items (one launch per step; the
     # encode is two launches, k_enc_count + k_encode, reported beside it).
     # traffic: PMC-measured HBM bytes per launch of the same kernel on the
     # same config (profiles/traffic.json, FETCH_SIZE x 2 + WRITE_SIZE per
     # MI355X_MICROARCH.md), when recorded for this batch size.
-    dec_alg = raw_bytes + enc_total + 12 * n  # reads E + offsets, writes R + status
-    enc_alg = raw_bytes + enc_total + 12 * n
+    # (per launch: the event pass's mean over the rotated batches)
+    alg = [r + e + 12 * k for r, e, k in zip(raws, enc_totals, ns)]  # reads E + offsets, writes R + status
+    dec_alg = int(round(np.mean([alg[i % nb] for i in range(KE)])))
+    enc_alg = dec_alg
     achieved = dec_alg / t_dec / 1e9
     copy_gbs = device_copy_gbs(torch, dev)
     roof = {"bound": "hbm", "kernel": "k_decode_items", "achieved": round(achieved, 2),
@@ -400,16 +470,16 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
 
     out = {"metric": "GB/s HPACK Huffman enc+dec (device-resident, batched headers)",
            "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
-           "steps": args.steps, "warmup": args.warmup,
+           "steps": steps, "warmup": args.warmup,
            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
            "scaling": scaling, "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (%s)" % data,
            "config": {"workload": CONFIG_NAMES[cfg], "config_id": cfg, "strings_per_gpu": n,
                       "raw_bytes_per_gpu": raw_bytes, "enc_bytes_per_gpu": enc_total,
                       "E_over_R": round(enc_total / max(1, raw_bytes), 4),
-                      "alg_bytes_per_step_all_gpus": int(B_total),
+                      "alg_bytes_per_step_all_gpus": int(round(B_total / steps)),
                       "parallelism": "shard%d (independent batches, no collective)" % world,
-                      "streams": len(pipes)},
+                      "streams": len(pipes), "batches": nb},
            "roofline": roof}
 
     if host_resident is None:
@@ -422,10 +492,11 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
         # pipes (one step's D2H overlaps the next step's H2D).
         h_src = torch.from_numpy(pool).pin_memory()
         h_off = torch.from_numpy(off.view(np.int32)).pin_memory()
-        dec_used = int(P0.dec_off[-1].item()) & 0xFFFFFFFF
-        for k, p in enumerate(pipes):
-            if k:
-                p.src, p.src_off = torch.empty_like(src), torch.empty_like(src_off)
+        P0.run(0)
+        torch.cuda.synchronize()
+        dec_used = int(P0.dec_off[n].item()) & 0xFFFFFFFF
+        for p in pipes:
+            p.host_src = (torch.empty_like(srcs[0]), torch.empty_like(srcs_off[0]))
             p.h_enc = torch.empty(enc_total + 16, dtype=torch.uint8).pin_memory()
             p.h_eoff = torch.empty(n + 1, dtype=torch.int32).pin_memory()
             p.h_dec = torch.empty(dec_used, dtype=torch.uint8).pin_memory()
@@ -434,13 +505,13 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
         def host_step(i):
             p = pipes[i % len(pipes)]
             with torch.cuda.stream(p.stream):
-                p.src.copy_(h_src, non_blocking=True)
-                p.src_off.copy_(h_off, non_blocking=True)
-                p.run()
+                p.host_src[0].copy_(h_src, non_blocking=True)
+                p.host_src[1].copy_(h_off, non_blocking=True)
+                p.run(0)
                 p.h_enc[:enc_total].copy_(p.enc[:enc_total], non_blocking=True)
-                p.h_eoff.copy_(p.enc_off, non_blocking=True)
+                p.h_eoff.copy_(p.enc_off[:n + 1], non_blocking=True)
                 p.h_dec.copy_(p.dec[:dec_used], non_blocking=True)
-                p.h_st.copy_(p.status, non_blocking=True)
+                p.h_st.copy_(p.status[:n], non_blocking=True)
 
         for i in range(max(1, args.warmup) * len(pipes)):
             host_step(i)
@@ -459,7 +530,7 @@ def run_roundtrip(args, torch, dist, nghttp2_amd, dev, world, allreduce, pool, o
             assert np.array_equal(p.h_st.numpy(), raw_len)
         pcie = (raw_bytes + 4 * (n + 1)) + (enc_total + 4 * (n + 1)) + dec_used + 4 * n
         out["host_resident"] = {
-            "value": round(B_rank * args.steps / th / 1e9, 3), "unit": "GB/s",
+            "value": round(B_b[0] * args.steps / th / 1e9, 3), "unit": "GB/s",
             "ms_per_step": round(th / args.steps * 1e3, 4),
             "pcie_bytes_per_step": pcie, "streams": len(pipes),
             "note": "pinned H2D raw+offsets, encode, decode, D2H encoded+offsets, "

@@ -450,6 +450,8 @@ typedef struct {
  * as nghttp2_amd_hd_deflate_hd2, the wire written across the chunks
  * vec[0..veclen) in order (each filled before the next); INSUFF_BUFSIZE when
  * their total is too small, including veclen == 0 and zero-length chunks.
+ * On INSUFF_BUFSIZE with several chunks, none of them is written (the
+ * reference leaves the bytes it had written before it ran out).
  */
 NGHTTP2_AMD_EXTERN ptrdiff_t nghttp2_amd_hd_deflate_hd_vec2(nghttp2_amd_hd_deflater *deflater,
                                                              const nghttp2_amd_vec *vec,

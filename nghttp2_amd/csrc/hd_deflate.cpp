@@ -27,6 +27,7 @@
 #include <deque>
 #include <unordered_map>
 #include <mutex>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -285,6 +286,7 @@ int nghttp2_amd_hd_deflate_blocks(nghttp2_amd_hd_deflater *const *deflaters, uin
     if (!deflaters[i] || block_nv_off[i] > block_nv_off[i + 1]) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
 
   using nghttp2_amd_host::parallel_for;
+  nghttp2_amd_host::Pool::CallScope scope;  // workers spin between this call's phases only
   nghttp2_amd_host::Phases ph("deflate");
   // ---- the token and hash of every field name of the batch (lookup_token,
   // name_hash; deflate_nv, lib/nghttp2_hd.c:1388-1393): one GPU launch over
@@ -600,15 +602,22 @@ ptrdiff_t nghttp2_amd_hd_deflate_hd_vec2(nghttp2_amd_hd_deflater *deflater, cons
     if (!vec[i].base && vec[i].len) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
     total += vec[i].len;
   }
-  // the wire into one contiguous buffer of the chunks' total, then across
-  // the chunks in order (nghttp2_bufs_wrap_init2 fills them one by one)
-  std::vector<uint8_t> tmp(total);
-  const ptrdiff_t n = nghttp2_amd_hd_deflate_hd2(deflater, tmp.data(), total, nva, nvlen, stream);
+  // one chunk: the wire straight into it
+  if (veclen == 1) return nghttp2_amd_hd_deflate_hd2(deflater, vec[0].base, vec[0].len, nva, nvlen, stream);
+  // else the wire into one contiguous scratch buffer, then across the chunks
+  // in order (nghttp2_bufs_wrap_init2 fills them one by one).  The scratch is
+  // not zero-filled and is capped at the list's bound (an output always fits
+  // that, so the cap changes no result).  On INSUFF_BUFSIZE the chunks are
+  // left untouched, where the reference leaves the bytes it had written.
+  const size_t cap = std::min(total, nghttp2_amd_hd_deflate_bound(deflater, nva, nvlen));
+  std::unique_ptr<uint8_t[]> tmp(new (std::nothrow) uint8_t[cap ? cap : 1]);
+  if (!tmp) return NGHTTP2_AMD_ERR_NOMEM;
+  const ptrdiff_t n = nghttp2_amd_hd_deflate_hd2(deflater, tmp.get(), cap, nva, nvlen, stream);
   if (n < 0) return n;
   size_t o = 0;
   for (size_t i = 0; i < veclen && o < (size_t)n; ++i) {
     const size_t k = std::min(vec[i].len, (size_t)n - o);
-    memcpy(vec[i].base, tmp.data() + o, k);
+    memcpy(vec[i].base, tmp.get() + o, k);
     o += k;
   }
   return n;

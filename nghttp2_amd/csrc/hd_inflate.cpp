@@ -642,6 +642,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   // engine's buffers are reused across calls, so a warm call allocates
   // nothing here
   using nghttp2_amd_host::parallel_for;
+  nghttp2_amd_host::Pool::CallScope scope;  // workers spin between this call's phases only
   nghttp2_amd_host::Phases ph("inflate");
   std::lock_guard<std::mutex> guard(engine().mu);
   Engine &E = engine();

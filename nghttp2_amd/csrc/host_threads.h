@@ -36,6 +36,13 @@ inline unsigned host_threads() {
   return t;
 }
 
+// A spin-wait hint for the busy loops below (x86 `pause`; a no-op elsewhere).
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#endif
+}
+
 class Pool {
  public:
   static Pool &get() {
@@ -44,30 +51,43 @@ class Pool {
   }
   unsigned workers() const { return (unsigned)th_.size(); }
   // Runs fn on every worker and on the caller; returns when all are done.
-  // Calls from several host threads take turns.  Workers spin for a short
-  // while (spin_us()) after each job before they park on the condition
-  // variable, so the several parallel phases of one front-end call hand
-  // work over without a futex wake-up each (round 5: the inflate call runs
-  // five such phases in well under a millisecond).
+  // Calls from several host threads take turns.
   void run(const std::function<void()> &fn) {
     std::lock_guard<std::mutex> turn(run_mu_);
-    job_.store(&fn, std::memory_order_relaxed);
-    active_.store((unsigned)th_.size(), std::memory_order_relaxed);
+    job_.v.store(&fn, std::memory_order_relaxed);
+    active_.v.store((unsigned)th_.size(), std::memory_order_relaxed);
     bool wake;
     {
       std::lock_guard<std::mutex> l(mu_);
-      gen_.fetch_add(1, std::memory_order_release);
+      gen_.v.fetch_add(1, std::memory_order_release);
       wake = sleepers_ > 0;
     }
     if (wake) cv_.notify_all();
     fn();
-    for (unsigned i = 0; active_.load(std::memory_order_acquire) != 0; ++i)
-      if (i > 4096) std::this_thread::yield();
-    job_.store(nullptr, std::memory_order_relaxed);
+    for (unsigned i = 0; active_.v.load(std::memory_order_acquire) != 0; ++i) {
+      if (i < 4096) cpu_relax();
+      else std::this_thread::yield();
+    }
+    job_.v.store(nullptr, std::memory_order_relaxed);
   }
+  // A front-end call that runs several parallel phases holds a CallScope for
+  // its whole duration: while one is open, a worker that finishes a phase
+  // spins (with a pause) for the next one, up to spin_us(), instead of
+  // parking on the condition variable, so the call's phases hand over without
+  // a futex wake-up each.  With no call open the workers park at once, so an
+  // embedding application's threads never compete with idle spinning
+  // (round 6; round 5 spun 200 us after every phase, call or not).
+  class CallScope {
+   public:
+    CallScope() { calls().v.fetch_add(1, std::memory_order_relaxed); }
+    ~CallScope() { calls().v.fetch_sub(1, std::memory_order_relaxed); }
+    CallScope(const CallScope &) = delete;
+    CallScope &operator=(const CallScope &) = delete;
+  };
 
  private:
-  // NGHTTP2_AMD_SPIN_US (default 200; 0: park at once, as before round 5)
+  // NGHTTP2_AMD_SPIN_US (default 200; 0: always park at once): the longest a
+  // worker spins between the phases of an open call
   static int spin_us() {
     static const int v = [] {
       const char *e = getenv("NGHTTP2_AMD_SPIN_US");
@@ -88,35 +108,47 @@ class Pool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      // spin for the next job for kSpinUs, then park
+      // spin for the next job while a call is open (at most spin_us()), then park
       bool got = false;
       const auto t0 = std::chrono::steady_clock::now();
-      for (unsigned i = 0; !got; ++i) {
-        if (gen_.load(std::memory_order_acquire) != seen) {
+      for (unsigned i = 0;; ++i) {
+        if (gen_.v.load(std::memory_order_acquire) != seen) {
           got = true;
           break;
         }
+        if (calls().v.load(std::memory_order_relaxed) == 0) break;
         if ((i & 255u) == 255u &&
             std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us()))
           break;
+        cpu_relax();
       }
       if (!got) {
         std::unique_lock<std::mutex> l(mu_);
         ++sleepers_;
-        cv_.wait(l, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+        cv_.wait(l, [&] { return gen_.v.load(std::memory_order_relaxed) != seen; });
         --sleepers_;
       }
-      seen = gen_.load(std::memory_order_acquire);
-      (*job_.load(std::memory_order_relaxed))();
-      active_.fetch_sub(1, std::memory_order_acq_rel);
+      seen = gen_.v.load(std::memory_order_acquire);
+      (*job_.v.load(std::memory_order_relaxed))();
+      active_.v.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
+  // (each shared word on its own cache line: the workers' decrements of
+  // active_ must not bounce the line the spinning workers poll gen_ on)
+  template <class T>
+  struct alignas(64) Line {
+    std::atomic<T> v{};
+  };
   std::vector<std::thread> th_;
   std::mutex run_mu_, mu_;
   std::condition_variable cv_;
-  std::atomic<const std::function<void()> *> job_{nullptr};
-  std::atomic<unsigned> active_{0};
-  std::atomic<uint64_t> gen_{0};
+  Line<const std::function<void()> *> job_;
+  Line<unsigned> active_;
+  Line<uint64_t> gen_;
+  static Line<int> &calls() {  // open CallScopes (no pool is started for one)
+    static Line<int> c;
+    return c;
+  }
   unsigned sleepers_ = 0;  // (under mu_)
 };
 
