@@ -1486,14 +1486,18 @@ struct LdsPtrSink {
 };
 typedef LdsPtrSink DISink;
 
-// the item decoder's 16-byte input loads and output stores
-// The item decoder's input loads are nontemporal (DD_NTL): the encoded pool
-// is read once, and the cache keeps the next step's raw input instead (bench,
-// one box, three alternations: event-timed encode 0.1376 vs 0.1452 ms, the
-// decode and the two-stream step equal; nontemporal output stores instead
-// took the decode from 0.209 to 0.374 ms)
+// The item decoder's 16-byte input loads (DD_NTL: nontemporal).  Round 5
+// made them nontemporal so that the cache kept the next step's raw input --
+// a benefit only of a bench that re-encodes the same batch every step.  On
+// the round-6 bench, which rotates three distinct batches, plain loads are
+// no slower (bench, 100 steps, three alternations: 1966.1 / 1965.3 / 1968.4
+// GB/s against 1958.2 / 1957.9 / 1952.7 nontemporal; with one batch 2029.0 /
+// 2019.1 / 2033.1 against 2019.2 / 2029.5 / 2029.0), and the 20-byte warm-up
+// overlaps of neighbouring rounds are served by the cache again instead of
+// HBM (profiles/r06/bench/ntl_*).  (Nontemporal output stores: 0.374 vs
+// 0.209 ms.)
 #ifndef DD_NTL
-#define DD_NTL 1
+#define DD_NTL 0
 #endif
 __device__ __forceinline__ uint4 dd_ld16(const uint4 *p) {
 #if DD_NTL

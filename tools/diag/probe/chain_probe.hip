@@ -45,6 +45,8 @@ namespace host {
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
 
 constexpr uint32_t IP = 40;          // item bytes
 constexpr uint32_t OB = 72;          // output region per item (di_rb(40))
@@ -61,7 +63,14 @@ struct Chain {
 };
 
 // W waves per workgroup, CH chains per lane, R repeats of the wave's round.
-template <int CH>
+// V (CH = 1 only; what the pair loop's LDS time goes to): 0 the product's
+// shape; 1 no output stores; 2 one dword store per pair (bytes gathered in a
+// 64-bit register, the dword stored when full); 3 lookups made bank-conflict
+// free (each lane of a 32-lane group on its own bank; wrong symbols, the
+// same step count on average); 4 no prefetch read of the next staged word;
+// 5 the pair's raw entries stored as one aligned 8-byte record; 6 its four
+// symbol bytes as one aligned 4-byte record (both: compaction not included)
+template <int CH, int V = 0>
 __global__ void k_probe(const uint32_t *__restrict__ enc_words, uint32_t nwords, uint32_t R,
                         uint32_t *__restrict__ out_bytes) {
   extern __shared__ uint32_t smem[];
@@ -95,28 +104,142 @@ __global__ void k_probe(const uint32_t *__restrict__ enc_words, uint32_t nwords,
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
-    if (CH == 1) {
+    if (CH == 1 && V >= 7) {
+      // V 7: the bytes of pair i gathered into a 64-bit register and stored
+      // as whole dwords, done while pair i + 1's first lookup is in flight
+      // (software-pipelined); V 8: the next staged words read two at a time,
+      // every second pair; V 9: both
       Chain<CH> &x = c[0];
+      uint64_t acc = 0;
+      uint32_t nb = 0, pe1 = 0, pe2 = 0, N1 = 0, par = 0;
+      lds_u32 *q = (lds_u32 *)x.p;
+      if (V >= 8) N1 = ib[(uint32_t)x.kw + 3u];
       while ((int32_t)x.nq >= x.nG) {
         const uint32_t w = __builtin_amdgcn_alignbit(x.A, x.B, x.nq);
         const uint32_t e1 = lut[w >> 19];
+        // (the gather below after the lookup's issue, not before it)
+        __builtin_amdgcn_sched_barrier(0);
+        if (V != 8) {
+          const uint32_t c1 = E_CNT8(pe1);
+          const uint32_t b = __builtin_amdgcn_perm(0u, pe1, 0x0C0C0200u) |
+                             (__builtin_amdgcn_perm(0u, pe2, 0x0C0C0200u) << c1);
+          acc |= (uint64_t)b << nb;
+          nb += c1 + E_CNT8(pe2);
+          *q = (uint32_t)acc;
+          const bool full = nb >= 32u;
+          q += full ? 1 : 0;
+          acc = full ? acc >> 32 : acc;
+          nb -= full ? 32u : 0u;
+        }
+        __builtin_amdgcn_sched_barrier(0);
         const uint32_t U1 = e1 ? E_USED(e1) : 13u;
         const uint32_t e2 = lut[(w << U1) >> 19];
         const uint32_t U2 = e2 ? E_USED(e2) : 13u;
-        x.p[0] = (uint8_t)e1;
-        x.p[1] = (uint8_t)(e1 >> 16);
-        x.p += E_CNT8(e1) >> 3;
-        x.p[0] = (uint8_t)e2;
-        x.p[1] = (uint8_t)(e2 >> 16);
-        x.p += E_CNT8(e2) >> 3;
+        if (V == 8) {
+          x.p[0] = (uint8_t)e1;
+          x.p[1] = (uint8_t)(e1 >> 16);
+          x.p += E_CNT8(e1) >> 3;
+          x.p[0] = (uint8_t)e2;
+          x.p[1] = (uint8_t)(e2 >> 16);
+          x.p += E_CNT8(e2) >> 3;
+        }
+        pe1 = e1;
+        pe2 = e2;
         const uint32_t u = U1 + U2;
         const bool t = u > (x.nq & 31u);
         x.nq -= u;
         x.A = t ? x.B : x.A;
         x.B = t ? x.N : x.B;
         x.kw += t ? 1 : 0;
-        x.N = ib[(uint32_t)x.kw + 2u];
+        if (V >= 8) {
+          // words kw + 2, kw + 3 held in N, N1; read two every second pair
+          // (two pairs cross at most two words: 52 bits)
+          x.N = t ? N1 : x.N;
+          par ^= 1u;
+          if (par == 0u) {
+            const uint32_t k2 = (uint32_t)x.kw + 2u;
+            x.N = ib[k2];
+            N1 = ib[k2 + 1u];
+          }
+        } else {
+          x.N = ib[(uint32_t)x.kw + 2u];
+        }
       }
+      if (V != 8) {
+        const uint32_t c1 = E_CNT8(pe1);
+        nb += c1 + E_CNT8(pe2);
+        x.p = (lds_u8 *)q + (nb >> 3);
+      }
+    } else     if (CH == 1) {
+      Chain<CH> &x = c[0];
+      uint64_t acc = 0;
+      uint32_t nb = 0, npair = 0;
+      while ((int32_t)x.nq >= x.nG) {
+        const uint32_t w = __builtin_amdgcn_alignbit(x.A, x.B, x.nq);
+        const uint32_t i1 = V == 3 ? (((w >> 19) & ~31u) | (lane & 31u)) : (w >> 19);
+        const uint32_t e1 = lut[i1];
+        const uint32_t U1 = e1 ? E_USED(e1) : 13u;
+        const uint32_t i2 = V == 3 ? ((((w << U1) >> 19) & ~31u) | (lane & 31u)) : ((w << U1) >> 19);
+        const uint32_t e2 = lut[i2];
+        const uint32_t U2 = e2 ? E_USED(e2) : 13u;
+        if (V == 1) {
+          x.p += (E_CNT8(e1) + E_CNT8(e2)) >> 3;
+        } else if (V == 10) {
+          // the pair's 2-4 symbol bytes packed and stored as one dword at the
+          // (unaligned) byte position; the next store overwrites the rest
+          const uint32_t c1 = E_CNT8(e1);
+          const uint32_t b = __builtin_amdgcn_perm(0u, e1, 0x0C0C0200u) |
+                             (__builtin_amdgcn_perm(0u, e2, 0x0C0C0200u) << c1);
+          *(lds_u32 *)x.p = b;
+          x.p += (c1 + E_CNT8(e2)) >> 3;
+        } else if (V == 11) {
+          // 4-byte record per pair (V 6) plus the two entries' symbol counts
+          // gathered in a 64-bit register, 4 bits a pair
+          *(lds_u32 *)(ob + OB * lane + 4u * (npair & 15u)) = __builtin_amdgcn_perm(e2, e1, 0x06040200u);
+          const uint32_t cc = ((e1 >> 13) & 3u) | (((e2 >> 13) & 3u) << 2);
+          acc |= (uint64_t)cc << (4u * (npair & 15u));
+          ++npair;
+          x.p += (E_CNT8(e1) + E_CNT8(e2)) >> 3;
+        } else if (V == 5 || V == 6) {
+          // the pair's two raw entries as one 8-byte record (compacted to
+          // bytes later, outside the loop); V 6: one 4-byte record (the
+          // symbol bytes, 0 and 2 of each entry)
+          if (V == 5) *(lds_u32x2 *)(ob + OB * lane + 8u * (npair & 7u)) = u32x2{e1, e2};
+          else *(lds_u32 *)(ob + OB * lane + 4u * (npair & 15u)) = __builtin_amdgcn_perm(e2, e1, 0x06040200u);
+          ++npair;
+          x.p += (E_CNT8(e1) + E_CNT8(e2)) >> 3;
+        } else if (V == 2) {
+          // both entries' bytes (0 and 2 of each) contiguous, then into acc
+          const uint32_t b1 = __builtin_amdgcn_perm(0u, e1, 0x0C0C0200u);
+          const uint32_t b2 = __builtin_amdgcn_perm(0u, e2, 0x0C0C0200u);
+          const uint32_t c1 = E_CNT8(e1);
+          const uint64_t b = (uint64_t)b1 | ((uint64_t)b2 << c1);
+          acc |= b << nb;
+          nb += c1 + E_CNT8(e2);
+          *(lds_u32 *)x.p = (uint32_t)acc;
+          const bool full = nb >= 32u;
+          x.p += full ? 4 : 0;
+          acc = full ? acc >> 32 : acc;
+          nb -= full ? 32u : 0u;
+        } else {
+          x.p[0] = (uint8_t)e1;
+          x.p[1] = (uint8_t)(e1 >> 16);
+          x.p += E_CNT8(e1) >> 3;
+          x.p[0] = (uint8_t)e2;
+          x.p[1] = (uint8_t)(e2 >> 16);
+          x.p += E_CNT8(e2) >> 3;
+        }
+        const uint32_t u = U1 + U2;
+        const bool t = u > (x.nq & 31u);
+        x.nq -= u;
+        x.A = t ? x.B : x.A;
+        x.B = t ? x.N : x.B;
+        x.kw += t ? 1 : 0;
+        if (V == 4) x.N = x.A ^ x.kw;
+        else x.N = ib[(uint32_t)x.kw + 2u];
+      }
+      if (V == 2) x.p += nb >> 3;
+      if (V == 11) total += (uint32_t)(acc >> 60);  // (keeps the mask live)
     } else {
       // both chains step together while either runs; a finished chain's
       // step takes no bits and its pointer does not move
@@ -227,6 +350,30 @@ int main(int argc, char **argv) {
            lds, best, bytes / 1e6, bytes / (best * 1e3), bytes / (best * 1e3) / (CH * W));
   };
   for (int W : {4, 8, 12, 16}) run(k_probe<1>, 1, W);
+  for (int W : {12, 16}) {
+    printf("variant 1 (no output stores): ");
+    run(k_probe<1, 1>, 1, W);
+    printf("variant 2 (one dword store per pair): ");
+    run(k_probe<1, 2>, 1, W);
+    printf("variant 3 (conflict-free lookups): ");
+    run(k_probe<1, 3>, 1, W);
+    printf("variant 4 (no prefetch read): ");
+    run(k_probe<1, 4>, 1, W);
+    printf("variant 5 (one 8-byte record per pair): ");
+    run(k_probe<1, 5>, 1, W);
+    printf("variant 6 (one 4-byte record per pair): ");
+    run(k_probe<1, 6>, 1, W);
+    printf("variant 10 (one unaligned dword store per pair): ");
+    run(k_probe<1, 10>, 1, W);
+    printf("variant 11 (4-byte record + count mask): ");
+    run(k_probe<1, 11>, 1, W);
+    printf("variant 7 (pipelined dword gather): ");
+    run(k_probe<1, 7>, 1, W);
+    printf("variant 8 (two-word refill every 2nd pair): ");
+    run(k_probe<1, 8>, 1, W);
+    printf("variant 9 (7 + 8): ");
+    run(k_probe<1, 9>, 1, W);
+  }
   for (int W : {4, 6, 8, 10}) run(k_probe<2>, 2, W);
   return 0;
 }
