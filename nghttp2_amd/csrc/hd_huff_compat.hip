@@ -16,6 +16,11 @@
 // a D2H copy around the kernels took 21.0 / 26.7 us per encode pair /
 // decode), then one synchronisation.
 //
+// Strings of kCopyMin bytes or more go the other way: the block is copied to
+// a device buffer, the kernels run there and the results are copied back --
+// for long strings one DMA copy each way beats many waves reading and writing
+// uncached host memory across PCIe (round 6, advisor).
+//
 // emit_string (lib/nghttp2_hd.c:1009, :1037) asks for the count and then,
 // when Huffman wins, for the encoding of the same bytes.  The count runs the
 // whole encode and keeps its output (and a copy of the input) in the
@@ -45,6 +50,8 @@ bool hip_ok(hipError_t e) {
 
 size_t round16(size_t x) { return (x + 15u) & ~size_t(15); }
 
+constexpr size_t kCopyMin = 64u << 10;  // string bytes from which a call copies instead of mapping
+
 // Layout of one call (device buffer and pinned block alike):
 //   [in: string bytes, round16(len) + 16][meta: 64 B][res: 16 B][out bytes]
 // meta: u32 src_off[2] | u32 dst_off[2] | u16 init fstate | u8 init flags
@@ -65,6 +72,8 @@ struct Engine {
   hipStream_t st = nullptr;
   uint8_t *d_buf = nullptr, *h_pin = nullptr;  // d_buf: h_pin's device address
   size_t cap = 0;
+  uint8_t *d_dev = nullptr;  // long strings: a device copy of the block
+  size_t dev_cap = 0;
   void *d_ws = nullptr;
   size_t ws = 0;
   // the last count's full encode (emit_string's count -> encode pair)
@@ -74,12 +83,13 @@ struct Engine {
   ~Engine() { release(); }
   void release() {
     if (h_pin) (void)hipHostFree(h_pin);
+    if (d_dev) (void)hipFree(d_dev);
     if (d_ws) (void)hipFree(d_ws);
     if (st) (void)hipStreamDestroy(st);
-    d_buf = h_pin = nullptr;
+    d_buf = h_pin = d_dev = nullptr;
     d_ws = nullptr;
     st = nullptr;
-    cap = ws = 0;
+    cap = ws = dev_cap = 0;
     ready = false;
   }
   // the thread's stream and buffers on its current device; grows to `need`
@@ -123,6 +133,29 @@ struct Engine {
     }
     return true;
   }
+  // The block the kernels of a call use: the mapped pinned block, or (a
+  // string of kCopyMin bytes or more) a device buffer that receives the
+  // block's input and metadata [0, res) by one copy.
+  uint8_t *stage(const Layout &l, size_t len) {
+    if (len < kCopyMin) return d_buf;
+    if (l.total > dev_cap) {
+      if (d_dev) (void)hipFree(d_dev);
+      d_dev = nullptr;
+      dev_cap = 0;
+      if (!hip_ok(hipMalloc((void **)&d_dev, l.total))) return nullptr;
+      dev_cap = l.total;
+    }
+    if (!hip_ok(hipMemcpyAsync(d_dev, h_pin, l.res, hipMemcpyHostToDevice, st))) return nullptr;
+    return d_dev;
+  }
+  // after the kernels: the results and output back into the pinned block
+  // (copied calls), then the one synchronisation
+  bool finish(const Layout &l, const uint8_t *d) {
+    if (d != d_buf &&
+        !hip_ok(hipMemcpyAsync(h_pin + l.res, d + l.res, l.total - l.res, hipMemcpyDeviceToHost, st)))
+      return false;
+    return hip_ok(hipStreamSynchronize(st));
+  }
 };
 
 Engine &eng() {
@@ -146,11 +179,12 @@ bool encode_one(Engine &e, const uint8_t *src, size_t len) {
   m[0] = 0;
   m[1] = (uint32_t)len;
   upload(e, l, src, len);
-  uint8_t *d = e.d_buf;
+  uint8_t *d = e.stage(l, len);
+  if (!d) return false;
   if (nghttp2_amd_hd_huff_encode_batch(d, reinterpret_cast<const uint32_t *>(d + l.meta), 1, d + l.out,
-                                       e.cap - l.out, reinterpret_cast<uint32_t *>(d + l.res), e.d_ws,
+                                       l.total - l.out, reinterpret_cast<uint32_t *>(d + l.res), e.d_ws,
                                        e.ws, e.st) != 0 ||
-      !hip_ok(hipStreamSynchronize(e.st)))
+      !e.finish(l, d))
     return false;
   const uint32_t *r = reinterpret_cast<const uint32_t *>(e.h_pin + l.res);
   if (r[1] > bound) return false;
@@ -225,13 +259,14 @@ nghttp2_ssize nghttp2_hd_huff_decode(nghttp2_hd_huff_decode_context *ctx, nghttp
   memcpy(m + 16, &ctx->fstate, 2);
   m[18] = ctx->flags;
   upload(e, l, src, srclen);
-  uint8_t *d = e.d_buf;
+  uint8_t *d = e.stage(l, srclen);
+  if (!d) return NGHTTP2_AMD_ERR_NOMEM;
   const uint32_t *dm = reinterpret_cast<const uint32_t *>(d + l.meta);
   if (nghttp2_amd_hd_huff_decode_fsm_batch(d, dm, 1, d + l.out, dm + 2, reinterpret_cast<int32_t *>(d + l.res),
                                            reinterpret_cast<uint16_t *>(d + l.res + 4), d + l.res + 6,
                                            reinterpret_cast<const uint16_t *>(d + l.meta + 16),
                                            d + l.meta + 18, 0, e.st) != 0 ||
-      !hip_ok(hipStreamSynchronize(e.st)))
+      !e.finish(l, d))
     return NGHTTP2_AMD_ERR_NOMEM;
   int32_t st;
   uint16_t fs;

@@ -141,6 +141,7 @@ struct nghttp2_amd_hd_inflater {
   size_t bufsize_max = kDefaultTable;           // ctx.hd_table_bufsize_max
   size_t settings_max = kDefaultTable;          // settings_hd_table_bufsize_max
   size_t min_max = UINT32_MAX;                  // min_hd_table_bufsize_max
+  size_t max_nl = 0, max_vl = 0;                // longest name / value ever inserted (bounds)
   bool expect_size = false;                     // NGHTTP2_HD_STATE_EXPECT_TABLE_SIZE
   bool bad = false;                             // ctx.bad
   uint64_t batch_gen = 0;                       // the inflate_blocks call that last grouped it
@@ -163,6 +164,8 @@ struct nghttp2_amd_hd_inflater {
     if (room > bufsize_max) return;
     table.push(n, nl, v, vl);
     bufsize += room;
+    max_nl = std::max(max_nl, nl);
+    max_vl = std::max(max_vl, vl);
   }
   size_t max_index() const { return table.count + kStaticLen; }  // get_max_index
 };
@@ -202,6 +205,10 @@ struct alignas(128) Block {  // (aligned as BlockOut)
   // the output bound's parts (pass 1): fields, bytes other than dynamic-table
   // references, and the number of those references
   uint64_t nv = 0, ar = 0, ndyn = 0;
+  // the longest name and value any literal of the block can emit (a Huffman
+  // one at its decode bound): with the table's and the static table's
+  // longest, they bound what a dynamic-table reference of the block emits
+  uint64_t lit_name = 0, lit_val = 0;
 };
 
 // One block's emitted fields: name\0value\0 runs in `bytes`.
@@ -274,15 +281,18 @@ bool hip_ok(hipError_t e, const char *what) {
 }
 
 // (pinned, mapped into the device's address space and coherent: the
-// zero-copy decode reads and writes these pools directly)
-bool grow_host(void **p, size_t *cap, size_t need) {
+// zero-copy decode reads and writes these pools directly; mapped = false: a
+// pool the device only reaches by DMA copies, plain pinned memory)
+bool grow_host(void **p, size_t *cap, size_t need, bool mapped = true) {
   if (need <= *cap) return true;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
   // (coherent: a non-coherent mapping measured the same, round 5,
   // profiles/r05/inflate/pin_modes.log)
-  if (!hip_ok(hipHostMalloc(p, need, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc")) return false;
+  if (!hip_ok(hipHostMalloc(p, need, mapped ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault),
+              "hipHostMalloc"))
+    return false;
   *cap = need;
   return true;
 }
@@ -372,6 +382,33 @@ size_t static_len(uint32_t idx, int which) {
   }();
   (void)init;
   return lens[idx][which];
+}
+// the static table's longest name and value
+size_t static_max(int which) {
+  static const size_t m[2] = {[] {
+                                size_t x = 0;
+                                for (uint32_t i = 0; i < kStaticLen; ++i) x = std::max(x, static_len(i, 0));
+                                return x;
+                              }(),
+                              [] {
+                                size_t x = 0;
+                                for (uint32_t i = 0; i < kStaticLen; ++i) x = std::max(x, static_len(i, 1));
+                                return x;
+                              }()};
+  return m[which];
+}
+// What one dynamic-table reference of block b can emit (name + value): any
+// entry it can reach is one in the table now or one the block inserts, whose
+// name is a literal's, a static entry's or an older entry's and whose value
+// is a literal's.  So the longest name / value inserted so far, the static
+// table's and the block's literals bound it -- and so does the table limit
+// (round 6: the limit alone made a table of UINT32_MAX bytes send every
+// block with a dynamic reference through the slow copy-and-replay path).
+uint64_t dyn_ref_bound(const nghttp2_amd_hd_inflater *c, uint64_t lit_name, uint64_t lit_val) {
+  const uint64_t lim = std::min<uint64_t>(std::max<size_t>({64u, c->settings_max, c->bufsize_max}), UINT32_MAX);
+  const uint64_t n = std::max<uint64_t>({c->max_nl, static_max(0), lit_name});
+  const uint64_t v = std::max<uint64_t>({c->max_vl, static_max(1), lit_val});
+  return std::min(lim, n + v);
 }
 
 // Pass 2 for one block against its inflater (in order within a connection):
@@ -690,6 +727,7 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       else
         ++nd;
     };
+    uint64_t ln = 0, lv = 0;
     for (const Op &op : bl[i].ops) {
       if (op.kind == Op::SIZE) continue;
       ++nv;
@@ -697,11 +735,18 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
       if (op.kind == Op::INDEXED) {
         ref(op.value, false);
       } else {
-        if (op.new_name) ar += lit_len(op.name);
-        else ref(op.value, true);
+        if (op.new_name) {
+          ar += lit_len(op.name);
+          ln = std::max(ln, lit_len(op.name));
+        } else {
+          ref(op.value, true);
+        }
         ar += lit_len(op.val);
+        lv = std::max(lv, lit_len(op.val));
       }
     }
+    bl[i].lit_name = ln;
+    bl[i].lit_val = lv;
     bl[i].nv = nv;
     bl[i].ar = ar;
     bl[i].ndyn = nd;
@@ -728,9 +773,12 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   // latencies) and its output is copied out;  NGHTTP2_AMD_INFLATE_ZC=1 also
   // writes the output through the mapped pool, 0 copies both ways.
   // (2: zero-copy in, the output copied out -- DMA lands it in whole lines)
+  // The mode is read once per process; tests/test_inflate_zc.py runs the
+  // RFC and random-connection cases under each mode in its own process.
   static const int zc_mode = [] {
     const char *e = getenv("NGHTTP2_AMD_INFLATE_ZC");
-    return e ? atoi(e) : 2;
+    const int m = e ? atoi(e) : 2;
+    return m == 0 || m == 1 ? m : 2;
   }();
   const bool zero_copy = zc_mode == 1, zero_in = zc_mode == 2;
   hipStream_t st = (hipStream_t)stream;
@@ -739,9 +787,11 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   const size_t out_bytes = nh ? nghttp2_amd_hd_huff_decode_bound(hb, nh) : 0;
   const size_t meta = 3u * ((size_t)nh + 1u) * sizeof(uint32_t);
   if (nh) {
-    if (!grow_host((void **)&E.h_pool, &E.h_cap, in_bytes) ||
-        !grow_host((void **)&E.h_out, &E.o_cap, out_bytes) ||
-        !grow_host((void **)&E.h_meta, &E.m_cap, meta))
+    // (the output pool is a D2H copy target unless the kernel writes it
+    // through the mapping, mode 1; the input pools are mapped unless mode 0)
+    if (!grow_host((void **)&E.h_pool, &E.h_cap, in_bytes, zc_mode != 0) ||
+        !grow_host((void **)&E.h_out, &E.o_cap, out_bytes, zero_copy) ||
+        !grow_host((void **)&E.h_meta, &E.m_cap, meta, zc_mode != 0))
       return NGHTTP2_AMD_ERR_NOMEM;
     if (!zero_copy && ((!zero_in && !grow_dev((void **)&E.d_in, &E.din_cap, in_bytes)) ||
                        !grow_dev((void **)&E.d_out, &E.dout_cap, out_bytes) ||
@@ -864,19 +914,23 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
   // A batch that outgrows the caller's buffers is cut at the first block
   // that does not fit, and the tables replayed up to there, from snapshots.
   // The snapshots (a copy of every table) are taken only when an upper bound
-  // of the output (pass 1's per-block parts, a dynamic-table reference at the
-  // larger of the longest static entry and the connection's table limit) can
-  // pass the caps.
+  // of the output (pass 1's per-block parts, a dynamic-table reference at
+  // dyn_ref_bound) can pass the caps.
   bool may_cut = false;
   {
+    std::vector<uint64_t> run_ln(conns.size(), 0), run_lv(conns.size(), 0);
     // (saturating: a table limit near SIZE_MAX must not wrap the bound)
     auto sat = [](uint64_t a, uint64_t b) -> uint64_t { return a > UINT64_MAX - b ? UINT64_MAX : a + b; };
     uint64_t nv_bound = 0, ar_bound = 0;
     for (uint32_t i = 0; i < nblocks && !may_cut; ++i) {
       const nghttp2_amd_hd_inflater *c = inflaters[i];
-      const uint64_t rm = std::min<uint64_t>(
-          std::max<size_t>({64u, c->settings_max, c->bufsize_max}), UINT32_MAX);
       const Block &b = bl[i];
+      // (a connection's earlier blocks of the batch insert before this one:
+      // their literals count too -- the running maxima below)
+      const uint32_t cn = c->batch_conn;
+      run_ln[cn] = std::max(run_ln[cn], b.lit_name);
+      run_lv[cn] = std::max(run_lv[cn], b.lit_val);
+      const uint64_t rm = dyn_ref_bound(c, run_ln[cn], run_lv[cn]);
       const uint64_t dyn = b.ndyn && rm > UINT64_MAX / b.ndyn ? UINT64_MAX : b.ndyn * rm;
       nv_bound += b.nv;
       ar_bound = sat(ar_bound, sat(b.ar, dyn));
@@ -898,7 +952,9 @@ int nghttp2_amd_hd_inflate_blocks(nghttp2_amd_hd_inflater *const *inflaters, uin
     uint32_t cut = nblocks;
     for (uint32_t i = 0; i < nblocks; ++i) {
       const Block &b = bl[i];
-      const uint64_t rm = std::min<uint64_t>(std::max<size_t>({64u, c->settings_max, c->bufsize_max}), UINT32_MAX);
+      // (bounds from the table as it is now: the earlier blocks' inserts
+      // are in it, and in max_nl / max_vl)
+      const uint64_t rm = dyn_ref_bound(c, b.lit_name, b.lit_val);
       const uint64_t ar_b = b.ndyn && rm > (UINT64_MAX - b.ar) / b.ndyn ? UINT64_MAX : b.ar + b.ndyn * rm;
       ds.block = i;
       if (ds.nv + b.nv <= nva_cap && ar_b <= arena_cap - ds.ar) {

@@ -108,3 +108,47 @@ def test_compat_bulk_vs_oracle(dev):
         assert ob.raw[:buf.last - ob_base] == rout
         assert bool(L.nghttp2_hd_huff_decode_failure_state(ctypes.byref(ctx))) == \
             O.failure_state(rctx)
+
+
+@pytest.mark.gpu
+def test_compat_long_strings_vs_oracle(dev):
+    """Strings on both sides of the drop-in's copy threshold (64 KiB: the
+    mapped block below it, a device copy from it on), whole and chunked,
+    bit-exact against the oracle."""
+    import nghttp2_amd
+    L = nghttp2_amd.lib()
+    u8p = ctypes.c_char_p
+    L.nghttp2_hd_huff_encode_count.restype = ctypes.c_size_t
+    L.nghttp2_hd_huff_encode_count.argtypes = [u8p, ctypes.c_size_t]
+    L.nghttp2_hd_huff_encode.argtypes = [ctypes.POINTER(Bufs), u8p, ctypes.c_size_t]
+    L.nghttp2_hd_huff_decode.restype = ctypes.c_ssize_t
+    L.nghttp2_hd_huff_decode.argtypes = [ctypes.POINTER(Ctx), ctypes.POINTER(Buf), u8p,
+                                         ctypes.c_size_t, ctypes.c_int]
+    rng = np.random.default_rng(0x10C)
+    for size in (65535, 65536, 65537, 300001, (1 << 20) + 7):
+        # mostly printable, some bytes of every value (long codes included)
+        raw = rng.choice(np.arange(32, 127, dtype=np.uint8), size=size)
+        raw[rng.integers(0, size, size=size // 50)] = rng.integers(0, 256, size=size // 50)
+        raw = raw.tobytes()
+        rv, ref = O.encode(raw)
+        assert L.nghttp2_hd_huff_encode_count(raw, len(raw)) == len(ref) == O.encode_count(raw)
+        mem = ctypes.create_string_buffer(len(ref) + 64)
+        ch = Chain()
+        base = ctypes.addressof(mem)
+        ch.buf = Buf(base, base + len(mem), base, base, base)
+        bufs = Bufs(ctypes.pointer(ch), ctypes.pointer(ch), None, len(mem), 1, 1, 1, 0)
+        assert L.nghttp2_hd_huff_encode(ctypes.byref(bufs), raw, len(raw)) == 0
+        assert mem.raw[:ch.buf.last - base] == ref, size
+        for cut in (len(ref), len(ref) // 3):  # whole, then two chunks
+            ctx = Ctx(0, 1)
+            ob = ctypes.create_string_buffer(len(ref) * 8 // 5 + 16)
+            ob_base = ctypes.addressof(ob)
+            buf = Buf(ob_base, ob_base + len(ob), ob_base, ob_base, ob_base)
+            r1 = L.nghttp2_hd_huff_decode(ctypes.byref(ctx), ctypes.byref(buf), ref[:cut], cut,
+                                          1 if cut == len(ref) else 0)
+            assert r1 == cut
+            if cut < len(ref):
+                r2 = L.nghttp2_hd_huff_decode(ctypes.byref(ctx), ctypes.byref(buf), ref[cut:],
+                                              len(ref) - cut, 1)
+                assert r2 == len(ref) - cut
+            assert ob.raw[:buf.last - ob_base] == raw, (size, cut)

@@ -277,6 +277,35 @@ def test_inflate_buffer_cut_rolls_back_cpu(nconn, per, cap):
         assert (st2[k - cut], f2[k - cut]) == refs[order[k]].inflate_block(blocks[k]), k
 
 
+@pytest.mark.parametrize("nconn,per,cap", [(40, 5, 6000), (1, 60, 800), (1, 60, 100000)])
+def test_inflate_cut_with_huge_table_limit_cpu(nconn, per, cap):
+    """As above with the SETTINGS table limit at 2^32 - 1 (the reference's
+    change_table_size case): a dynamic reference's output is bounded by the
+    longest entry and literal, not by the limit (csrc/hd_inflate.cpp
+    dyn_ref_bound), so one connection's blocks take the direct replay; the
+    results and the cut are the oracle's either way."""
+    import nghttp2_amd
+    from nghttp2_amd import hd
+    order, blocks = _plain_batch(0xB1F, nconn, per)
+    infs = [nghttp2_amd.HpackInflater() for _ in range(nconn)]
+    refs = [HO.Inflater() for _ in range(nconn)]
+    for i, r in zip(infs, refs):
+        i.change_table_size(2**32 - 1)
+        r.change_table_size(2**32 - 1)
+    st, f = nghttp2_amd.inflate_blocks([infs[c] for c in order], blocks, arena_cap=cap, retry=False)
+    cut = st.index(hd.NGHTTP2_ERR_BUFFER_ERROR) if hd.NGHTTP2_ERR_BUFFER_ERROR in st else len(blocks)
+    assert all(s == hd.NGHTTP2_ERR_BUFFER_ERROR for s in st[cut:])
+    for k in range(cut):
+        assert (st[k], f[k]) == refs[order[k]].inflate_block(blocks[k]), k
+    for c in range(nconn):
+        assert infs[c].dynamic_table() == [tuple(e) for e in refs[c].table], c
+    if cut < len(blocks):
+        st2, f2 = nghttp2_amd.inflate_blocks([infs[c] for c in order[cut:]], blocks[cut:],
+                                             arena_cap=cap)
+        for k in range(cut, len(blocks)):
+            assert (st2[k - cut], f2[k - cut]) == refs[order[k]].inflate_block(blocks[k]), k
+
+
 # ---- the dynamic table's byte ring (csrc/hd_inflate.cpp DynTable): long
 # runs that wrap it many times, size updates that shrink and regrow it, and
 # an insertion whose name comes from the entry it evicts ----
