@@ -1390,6 +1390,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_IP40
 #define DD_IP40 40u  // piece bytes of the long-string instance
 #endif
+#ifndef DD_IP64
+#define DD_IP64 64u  // piece bytes of the short-string instance
+#endif
 #ifndef DD_TS64
 #define DD_TS64 64u  // strings per task unit of the 64-byte instance
 #endif
@@ -2445,7 +2448,7 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
   if ((fstate == nullptr) != (flags == nullptr)) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   if ((uint64_t)dst_cap > 0xFFFFFFFFull) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;  // uint32 offsets
   if (enc_bytes <= 48ull * n)
-    launch_decode_items<64u, DD_IW64, DD_LB64, DD_BI64, DD_SK64, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
+    launch_decode_items<DD_IP64, DD_IW64, DD_LB64, DD_BI64, DD_SK64, DD_TS64, DD_TK64>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   else
     launch_decode_items<DD_IP40, DD_IW40, DD_LB40, DD_BI40, DD_SK40, DD_TS40, DD_TK40>(src, src_off, n, dst, dst_cap, dst_off, status, fstate, flags, st);
   return hip_rv(hipGetLastError());
