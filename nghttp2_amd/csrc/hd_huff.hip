@@ -1391,7 +1391,13 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #define DD_IP40 40u  // piece bytes of the long-string instance
 #endif
 #ifndef DD_IP64
-#define DD_IP64 64u  // piece bytes of the short-string instance
+// piece bytes of the short-string instance.  Round 6: 96 (was 64): a string
+// of 65-96 encoded bytes is one item instead of two, so a task of short
+// strings with a few such strings among them needs one budgeted round, not a
+// second one for the leftover pieces (config 5, whose adversarial strings
+// reach 83 bytes: 98.7 -> 59.9 us; config 2, all <= 64 bytes: 43.6 / 43.7;
+// 128: 60.1 / 44.2; profiles/r06/ab/ab_piece96.log)
+#define DD_IP64 96u
 #endif
 #ifndef DD_TS64
 #define DD_TS64 64u  // strings per task unit of the 64-byte instance

@@ -267,7 +267,8 @@ class HuffmanBatchCodec:
         picks the kernel instance by the mean string length; when it is not
         given it is read from src_off on the call's stream (a host
         synchronisation of that stream: pass it to keep the call
-        asynchronous).  pick = "items64" / "pieces40" forces one instance
+        asynchronous).  pick = "items64" (the short-string instance: whole
+        strings of up to 96 bytes as one item since round 6) / "pieces40" forces one instance
         through that same argument (tests).  Returns
         (dst, dst_off, status[, fstate, flags])."""
         torch = self.torch

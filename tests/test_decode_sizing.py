@@ -28,7 +28,7 @@ def di_ibw(span):  # staged dwords
     return (((span + DD_OV + 64) // 4 + 8) + 3) & ~3
 
 
-INSTANCES = [(64, 0), (40, 0), (32, 0), (64, 2048), (64, 2304), (32, 1280)]
+INSTANCES = [(64, 0), (40, 0), (32, 0), (64, 2048), (64, 2304), (96, 2304), (128, 2304), (32, 1280)]
 
 
 def _rounds(sizes, ip, bi):
