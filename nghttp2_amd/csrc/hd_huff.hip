@@ -313,6 +313,74 @@ __device__ __forceinline__ uint32_t prefix7_byte(uint32_t n, uint32_t h, uint32_
 // A or past Z in the edge chunks add the same amount to both ends.
 // FR (emit_string, lib/nghttp2_hd.c:1001-1044): the tile sums are of the
 // string LITERALS' bytes, prefix7_len(P) + P with P = min(E, R) (H = E < R).
+// The code bits of a wave's 64 strings (string l in lane l: bytes [a_l,
+// b_l)): each lane sums its aligned 16-byte chunk's code lengths (lenT in
+// LDS, one byte per entry) and writes its in-chunk prefixes (16 bits a byte)
+// to the wave's LDS scratch pr (512 words); one wave scan places the chunks,
+// and every string lane reads P at its two ends.  Shared by k_enc_count and
+// the single-tile k_encode.
+__device__ __forceinline__ uint32_t wave_string_bits(const uint8_t *__restrict__ src, uint32_t a_l,
+                                                     uint32_t b_l, bool sl, uint32_t nstr,
+                                                     const lds_u8 *lenT, lds_u32 *pr, uint32_t lane) {
+  const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
+  const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
+  const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
+  const lds_u16 *pr16 = (const lds_u16 *)pr;
+  uint32_t Rc = 0, Pa = 0, Pb = 0;
+  bool ga = false, gb = false;
+  // chunks are loaded EC_CNT_PFD rounds ahead
+  uint4 q[EC_CNT_PFD];
+#pragma unroll
+  for (uint32_t d = 0; d < EC_CNT_PFD; ++d) {
+    q[d] = make_uint4(0, 0, 0, 0);
+    if (c0 + 64u * d + lane < c_end) q[d] = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u * d + lane) << 4));
+  }
+  for (uint32_t cb = c0; cb < c_end; cb += 64u) {
+    const uint32_t base = cb << 4;
+    const uint32_t wd[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
+#pragma unroll
+    for (uint32_t d = 0; d + 1 < EC_CNT_PFD; ++d) q[d] = q[d + 1];
+    q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
+    if (cb + 64u * EC_CNT_PFD + lane < c_end)
+      q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
+    uint32_t run = 0, pk[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t L = lenT[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+      if (j & 1) pk[j >> 1] |= run << 16; else pk[j >> 1] = run;
+      run += L;
+    }
+    u32x4 v0, v1;
+    v0.x = pk[0]; v0.y = pk[1]; v0.z = pk[2]; v0.w = pk[3];
+    v1.x = pk[4]; v1.y = pk[5]; v1.z = pk[6]; v1.w = pk[7];
+    *(lds_u32x4 *)(pr + 8u * lane) = v0;
+    *(lds_u32x4 *)(pr + 8u * lane + 4u) = v1;
+    const uint32_t Sinc = wave_incl_scan(run), Sx = Sinc - run;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the string ends in this round: P = chunk start + in-chunk prefix
+    const uint32_t ra = a_l - base, rb = b_l - base;
+    const uint32_t xa = __shfl(Sx, (ra >> 4) & 63u, 64), xb = __shfl(Sx, (rb >> 4) & 63u, 64);
+    if (sl && ra < 1024u) {
+      Pa = Rc + xa + pr16[ra];
+      ga = true;
+    }
+    if (sl && rb < 1024u) {
+      Pb = Rc + xb + pr16[rb];
+      gb = true;
+    }
+    Rc += __builtin_amdgcn_readlane(Sinc, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // an end at the last chunk's end (Z on a chunk boundary)
+  if (!ga) Pa = Rc;
+  if (!gb) Pb = Rc;
+  return sl ? Pb - Pa : 0u;
+}
+
 // k_enc_count: strings per wave (a tile of 256 is 256 / SPW waves); 32 / 16
 // measured slower (config 3 encode pair 137.5 / 146.3 vs 135.8 us)
 #define EC_CNT_SPW 64u
@@ -338,64 +406,8 @@ __global__ __launch_bounds__(EC_CNT_NT) void k_enc_count(const uint8_t *__restri
     const bool sl = lane < nstr;
     const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
     huge = b_l - a_l > NGHTTP2_AMD_ENCODE_MAX_STRING;
-    const uint32_t A = __builtin_amdgcn_readfirstlane(a_l);
-    const uint32_t Z = __builtin_amdgcn_readlane(b_l, nstr - 1u);
-    const uint32_t c0 = A >> 4, c_end = (Z + 15u) >> 4;
-    lds_u32 *pr = (lds_u32 *)pre[wv];
-    const lds_u16 *pr16 = (const lds_u16 *)pre[wv];
-    uint32_t Rc = 0, Pa = 0, Pb = 0;
-    bool ga = false, gb = false;
-    // chunks are loaded EC_CNT_PFD rounds ahead
-    uint4 q[EC_CNT_PFD];
-#pragma unroll
-    for (uint32_t d = 0; d < EC_CNT_PFD; ++d) {
-      q[d] = make_uint4(0, 0, 0, 0);
-      if (c0 + 64u * d + lane < c_end) q[d] = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u * d + lane) << 4));
-    }
-    for (uint32_t cb = c0; cb < c_end; cb += 64u) {
-      const uint32_t base = cb << 4;
-      const uint32_t wd[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
-#pragma unroll
-      for (uint32_t d = 0; d + 1 < EC_CNT_PFD; ++d) q[d] = q[d + 1];
-      q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
-      if (cb + 64u * EC_CNT_PFD + lane < c_end)
-        q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
-      uint32_t run = 0, pk[8];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t L = lenT[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-        if (j & 1) pk[j >> 1] |= run << 16; else pk[j >> 1] = run;
-        run += L;
-      }
-      u32x4 v0, v1;
-      v0.x = pk[0]; v0.y = pk[1]; v0.z = pk[2]; v0.w = pk[3];
-      v1.x = pk[4]; v1.y = pk[5]; v1.z = pk[6]; v1.w = pk[7];
-      *(lds_u32x4 *)(pr + 8u * lane) = v0;
-      *(lds_u32x4 *)(pr + 8u * lane + 4u) = v1;
-      const uint32_t Sinc = wave_incl_scan(run), Sx = Sinc - run;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // the string ends in this round: P = chunk start + in-chunk prefix
-      const uint32_t ra = a_l - base, rb = b_l - base;
-      const uint32_t xa = __shfl(Sx, (ra >> 4) & 63u, 64), xb = __shfl(Sx, (rb >> 4) & 63u, 64);
-      if (sl && ra < 1024u) {
-        Pa = Rc + xa + pr16[ra];
-        ga = true;
-      }
-      if (sl && rb < 1024u) {
-        Pb = Rc + xb + pr16[rb];
-        gb = true;
-      }
-      Rc += __builtin_amdgcn_readlane(Sinc, 63);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // an end at the last chunk's end (Z on a chunk boundary)
-    if (!ga) Pa = Rc;
-    if (!gb) Pb = Rc;
-    const uint32_t bits = sl ? Pb - Pa : 0u;
+    const uint32_t bits = wave_string_bits(src, a_l, b_l, sl, nstr, (const lds_u8 *)lenT,
+                                           (lds_u32 *)pre[wv], lane);
     e = (bits + 7u) >> 3;
     if (sl && out_len) out_len[t0 + lane] = bits_out ? bits : e;
     if (FR && sl) {
@@ -489,7 +501,11 @@ __device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, ui
 // and the pads' ones are OR'ed in by the string's own lane.  Extras reach
 // tens of bits, so FR combines codes in 64-bit pairs (not 32-bit pairs and
 // quads) and keeps the per-byte extras as u16.
-template <bool FR>
+// ONE: a batch of one tile (n <= 256) in a single launch -- the code bits
+// and the tile's total are counted in this workgroup first (the count
+// kernel's wave loop, its LDS scratch in the image), so a small batch (the
+// drop-in's single string, a deflater's header list) pays one launch, not two
+template <bool FR, bool ONE = false>
 __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict__ src,
                                                const uint32_t *__restrict__ off, uint32_t n,
                                                uint8_t *__restrict__ dst, uint64_t dst_cap,
@@ -504,17 +520,37 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   __shared__ uint32_t rawm[ENC_WAVES][FR ? 32 : 1];       // FR: a round's raw-string bytes
   __shared__ uint32_t o_sh[WG + 1];
   __shared__ uint32_t red[2 * (WG / 64)];
+  __shared__ uint8_t lenT1[ONE ? 256 : 1];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   // every load of the prologue is issued before any is used, so a tile's
   // start costs one memory latency (round 5: the staging, the offsets, the
   // tile sums and the tile's own sum waited in turn)
   const uint32_t s_me = blockIdx.x * WG + threadIdx.x;
-  const uint32_t bits_me = s_me < n ? dst_off[s_me] : 0u;
   const uint32_t t0 = blockIdx.x * WG + 64u * wv;
   const uint32_t nstr = t0 < n ? min(n - t0, 64u) : 0u;
   const bool sl = lane < nstr;
   const uint32_t a_l = sl ? off[t0 + lane] : 0u, b_l = sl ? off[t0 + lane + 1] : 0u;
-  const uint32_t tsum = tile_sums[blockIdx.x];
+  uint32_t bits_me, tsum;
+  if constexpr (ONE) {
+    lenT1[threadIdx.x] = dev::hd_huff_enc_len[threadIdx.x];
+    __syncthreads();
+    bits_me = nstr ? wave_string_bits(src, a_l, b_l, sl, nstr, (const lds_u8 *)lenT1,
+                                      (lds_u32 *)image[wv], lane)
+                   : 0u;
+    // the tile's total and its poison, as k_enc_count computes them
+    uint32_t e1 = (bits_me + 7u) >> 3;
+    if (FR && sl) {
+      const uint32_t R = b_l - a_l, P = e1 < R ? e1 : R;
+      e1 = prefix7_len(P) + P;
+    }
+    const bool huge = b_l - a_l > NGHTTP2_AMD_ENCODE_MAX_STRING;
+    uint32_t tot1, hi1;
+    block_excl_scan_sum<WG>(sl ? e1 : 0u, huge ? 0x2000u : (sl ? e1 : 0u) >> 16, red, &tot1, &hi1);
+    tsum = hi1 >= 0x2000u - WG ? 0xFFFFFFFFu : tot1;
+  } else {
+    bits_me = s_me < n ? dst_off[s_me] : 0u;
+    tsum = tile_sums[blockIdx.x];
+  }
   const uint32_t cc = dev::hd_huff_enc_code[threadIdx.x], cl = dev::hd_huff_enc_len[threadIdx.x];
   // the tile's offset: the tile totals before it (k_enc_count; 16 KB for 1M
   // strings, L2-resident), in 64 bits (a batch's encoded total may pass the
@@ -2528,6 +2564,11 @@ int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, const uint32_t *src_off
   if (workspace_size < nghttp2_amd_hd_huff_workspace_size(n))
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
+  if (nt == 1) {  // one tile: count and pack in one launch
+    hipLaunchKernelGGL((k_encode<false, true>), dim3(1), dim3(WG), 0, st, src, src_off, n, dst,
+                       (uint64_t)dst_cap, dst_off, (const uint32_t *)nullptr, (const uint64_t *)nullptr);
+    return hip_rv(hipGetLastError());
+  }
   uint32_t *tiles = (uint32_t *)workspace;
   hipLaunchKernelGGL(k_enc_count<false>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
   const uint64_t *pre = scan_tile_prefix(tiles, nt, workspace, st);
@@ -2564,6 +2605,11 @@ int nghttp2_amd_hd_emit_strings_batch(const uint8_t *src, const uint32_t *src_of
       dst_cap < nghttp2_amd_hd_emit_strings_bound(raw_bytes, n))
     return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
   const uint32_t nt = ntiles_for(n);
+  if (nt == 1) {  // one tile: count and pack in one launch
+    hipLaunchKernelGGL((k_encode<true, true>), dim3(1), dim3(WG), 0, st, src, src_off, n, dst,
+                       (uint64_t)dst_cap, dst_off, (const uint32_t *)nullptr, (const uint64_t *)nullptr);
+    return hip_rv(hipGetLastError());
+  }
   uint32_t *tiles = (uint32_t *)workspace;
   hipLaunchKernelGGL(k_enc_count<true>, dim3(nt), dim3(EC_CNT_NT), 0, st, src, src_off, n, dst_off, tiles, 1);
   const uint64_t *pre = scan_tile_prefix(tiles, nt, workspace, st);

@@ -127,6 +127,24 @@ def test_batch_sizes(codec, dev, n):
     check_roundtrip(codec, dev, pool, off, "pseudo n=%d" % n)
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 200, 255, 256, 257, 300])
+def test_single_tile_one_launch(codec, dev, n):
+    """A batch of at most 256 strings (one tile) is counted and packed in one
+    launch (k_encode<FR, ONE>): encode and string literals on both sides of
+    the threshold, with empty strings, every byte value (codes to 30 bits),
+    long strings and multi-byte literal lengths among them."""
+    rng = np.random.Generator(np.random.PCG64(0x1E + n))
+    strs = [b"", bytes(range(256)), b"\xff" * 127, b"a" * 128, b"0" * 16600]
+    strs += [bytes(rng.integers(0, 256, size=int(k), dtype=np.uint8))
+             for k in rng.integers(0, 300, size=max(0, n - len(strs)))]
+    strs = strs[:n]
+    off = np.zeros(len(strs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(x) for x in strs])
+    pool = np.frombuffer(b"".join(strs), dtype=np.uint8)
+    check_roundtrip(codec, dev, pool, off, "one tile n=%d" % n)
+    check_emit(codec, dev, pool, off, "one tile n=%d" % n)
+
+
 def test_all_byte_values(codec, dev):
     from nghttp2_amd import workloads as W
     pool, off = W.gen_all_bytes(30000, seed=5)
