@@ -151,7 +151,8 @@ NGHTTP2_AMD_EXTERN int nghttp2_amd_hd_huff_encode_batch(const uint8_t *src, cons
  * header blocks in wire order.  Two launches: the encode count (code bits
  * per string, tile sums of the literal lengths) and the encode pack, which
  * writes every literal -- prefix and payload -- straight into dst (no
- * intermediate Huffman pool).
+ * intermediate Huffman pool); a batch of at most 256 strings takes one
+ * launch that does both (the workspace is then not touched).
  *
  *   raw_bytes : src_off[n] - src_off[0] (sizes the bounds below)
  *   dst_cap   : >= nghttp2_amd_hd_emit_strings_bound(raw_bytes, n)
