@@ -102,7 +102,7 @@ for cfg in [int(c) for c in sys.argv[1:]] or [3, 2, 5]:
         same[k] = all(torch.equal(x, y) for x, y in zip(ref, cur))
     out = {"config": cfg, "n": n, "E": E, "decode_same": same,
            "decode": {} if os.environ.get("SKIP_DECODE") else timed(dec, list(libs))}
-    if src is not None:
+    if src is not None and not os.environ.get("SKIP_ENCODE"):
         ecap = codec.encode_bound(int(off[-1]), n)
         edst = torch.empty(ecap, dtype=torch.uint8, device=dev)
         eoff = torch.empty(n + 1, dtype=torch.int32, device=dev)
