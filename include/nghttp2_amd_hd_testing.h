@@ -34,6 +34,15 @@ NGHTTP2_AMD_EXTERN void nghttp2_amd_hd__set_gpu_names_min(uint32_t n);
 NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__copy_calib(void *dst, const void *src, size_t bytes,
                                                   void *stream);
 
+/* Bounds-checked debug build (the library compiled with HD_BOUNDS=1,
+ * lib/libnghttp2_amd_hd_bounds.so): waits for the device, then reports in
+ * *site the first out-of-bounds index the hot-path kernels recorded since
+ * the last call (0: none; 0x1xx encode, 0x2xx decode -- the sites are listed
+ * in DESIGN.md) and clears the record; *site == 0x5E1F7E57 on entry first
+ * runs a self-test kernel that records site 0x1FF.  Returns 0, a negative
+ * error, or 1 in the product build, which compiles no checks. */
+NGHTTP2_AMD_EXTERN int nghttp2_amd_hd__bounds_check(uint32_t *site);
+
 #ifdef __cplusplus
 }
 #endif

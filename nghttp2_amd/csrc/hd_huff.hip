@@ -66,6 +66,31 @@ namespace host {
 #define DEC_WG_PER_CU 8 // persistent decode grid: 256 CUs x 8 workgroups
 #define NUM_CU 256
 
+// Bounds-checked debug build (HD_BOUNDS=1; built beside the product as
+// lib/libnghttp2_amd_hd_bounds.so, run by tests/test_bounds_gpu.py): every
+// LDS staging, region and image index and every per-string global index the
+// hot-path kernels compute is checked against its buffer, and a violation
+// records its site in this translation unit's g_hd_bounds (one word per
+// lane, plain vector stores; nghttp2_amd_hd__bounds_check reports the first
+// nonzero word and clears them).  In the product (0) the checks compile to
+// nothing.
+#ifndef HD_BOUNDS
+#define HD_BOUNDS 0
+#endif
+#if HD_BOUNDS
+static __device__ uint32_t g_hd_bounds[64];
+#define HD_CHECK(ok, site)                                              \
+  do {                                                                  \
+    if (!(ok)) g_hd_bounds[threadIdx.x & 63u] = (uint32_t)(site);       \
+  } while (0)
+#define HD_LIM(x) , (x)
+#else
+#define HD_CHECK(ok, site) \
+  do {                     \
+  } while (0)
+#define HD_LIM(x)
+#endif
+
 #define HUFF_ACCEPTED 0x01u
 #define HUFF_SYM 0x02u
 #define FAIL_STATE 0x100u
@@ -482,7 +507,10 @@ __global__ __launch_bounds__(1024) void k_tile_prefix64(const uint32_t *__restri
 #define EC_RW_F (EC_RW + 112u)
 
 // OR the MSB-aligned bits {hi, lo} into the image at bit b
-__device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, uint32_t lo) {
+__device__ __forceinline__ void ec_or3(lds_u32 *img, uint32_t b, uint32_t hi, uint32_t lo,
+                                       uint32_t rw = 0xFFFFFFFFu) {
+  HD_CHECK((b >> 5) + 2u < rw, 0x101u);
+  (void)rw;
   const uint32_t o = b & 31u;
   lds_u32 *q = img + (b >> 5);
   atomicOr((uint32_t *)&q[0], hi >> o);
@@ -778,7 +806,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
         uint32_t b = ib0;
 #pragma unroll
         for (int m = 0; m < (FR ? 8 : 4); ++m) {
-          ec_or3(img, b, qh[m], qo[m]);
+          ec_or3(img, b, qh[m], qo[m], RW);
           b += ql[m];
         }
       } else {  // a code of <= 37 bits, MSB-aligned in 64; one dword at a time
@@ -798,10 +826,10 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
             if (FR) {
               const bool raw = (rm >> (4u * m + u)) & 1u, skip = (km >> (4u * m + u)) & 1u;
               const uint32_t xw = u < 2 ? pwf : pw2;
-              ec_or3(img, b, skip ? 0u : raw ? b8 << 21 : cj.x, 0u);
+              ec_or3(img, b, skip ? 0u : raw ? b8 << 21 : cj.x, 0u, RW);
               b += (skip ? 0u : raw ? 8u : cj.y) + ((xw >> (16 * (u & 1))) & 0xFFFFu);
             } else {
-              ec_or3(img, b, cj.x, 0u);
+              ec_or3(img, b, cj.x, 0u, RW);
               b += cj.y + ((pw >> (8 * u)) & 0xFFu);
             }
           }
@@ -812,6 +840,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     // ---- EOS-prefix padding (all ones) of the strings that end in this round
     if (tl) {
       const uint32_t r = (uint32_t)((olast_l >> 2) - WB) + EC_M;
+      HD_CHECK(r < RW, 0x102u);
       atomicOr((uint32_t *)&img[r], ((1u << pad_l) - 1u) << (24u - 8u * (olast_l & 3u)));
     }
     // ---- (FR) the literal prefixes attached in this round: H bit and the
@@ -821,6 +850,7 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
       for (uint32_t r = 0; r < PL_me; ++r) {
         const uint32_t q = o_me + r;
         const uint32_t v = prefix7_byte(P_me, H_me ? 1u : 0u, r);
+        HD_CHECK((uint32_t)((q >> 2) - WB) + EC_M < RW, 0x103u);
         atomicOr((uint32_t *)&img[(uint32_t)((q >> 2) - WB) + EC_M], v << (24u - 8u * (q & 3u)));
       }
     }
@@ -836,6 +866,8 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     const uint32_t ilo = (uint32_t)(((uint64_t)OA + 3u) / 4u - min(WB, ((uint64_t)OA + 3u) / 4u));
     const uint32_t ihi = (uint32_t)((uint64_t)OZ / 4u > WB ? (uint64_t)OZ / 4u - WB : 0u);
     uint8_t *const dw = dst + 4ull * WB;  // (uniform)
+    HD_CHECK(EC_M + nw <= RW, 0x104u);
+    HD_CHECK(ihi <= ilo || 4ull * (WB + ihi) <= dst_cap, 0x105u);
     for (uint32_t i = lane; i < nst; i += 64u) {
       const uint32_t v = __builtin_bswap32(img[EC_M + i]);
       img[EC_M + i] = 0u;
@@ -1512,12 +1544,20 @@ struct DiscardSink {  // a warm-up: its symbols belong to the item before
 // than base + count).
 struct LdsPtrSink {
   lds_u8 *p, *base;
+#if HD_BOUNDS
+  lds_u8 *lim;  // the lane's region end
+  __device__ __forceinline__ LdsPtrSink(lds_u8 *b, lds_u8 *l) : p(b), base(b), lim(l) {}
+#else
   __device__ __forceinline__ LdsPtrSink(lds_u8 *b) : p(b), base(b) {}
+#endif
   __device__ __forceinline__ uint32_t count() const { return (uint32_t)(p - base); }
   __device__ __forceinline__ void put_nf(uint32_t v, uint32_t c8) {
     // (round 3: one ds_write_b16 at the byte address -- the LDS runs in
     // unaligned mode, tools/diag/probe -- measured slower: 354.9 vs 296.2 us
     // on config 3, the hardware splits misaligned stores)
+#if HD_BOUNDS
+    HD_CHECK(p + 2 <= lim, 0x203u);
+#endif
     p[0] = (uint8_t)v;
     p[1] = (uint8_t)(v >> 16);
     p += c8 >> 3;
@@ -1563,7 +1603,15 @@ __device__ __forceinline__ uint32_t dd_win(const lds_u32 *ib, uint32_t q) {
 // Input word k (big-endian) of a decode: the wave's staged LDS copy.
 struct LdsIn {
   const lds_u32 *ib;
+#if HD_BOUNDS
+  uint32_t nw;  // staged words readable from ib (index -1 is the word before them)
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    HD_CHECK(k + 1u <= nw || k == 0xFFFFFFFFu, 0x202u);
+    return ib[k];
+  }
+#else
   __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return ib[k]; }
+#endif
 };
 
 struct DDRun {
@@ -1893,6 +1941,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
   // (budgeted rounds: the lane's output region moves with the round)
   lds_u8 *my_ob = (lds_u8 *)S.ob[wv] + lane * di_rb(IP);
   const lds_u32 *my_ob32 = (const lds_u32 *)my_ob;
+  [[maybe_unused]] uint32_t my_rb = di_rb(IP);  // (HD_BOUNDS) the region's bytes
   if (threadIdx.x == 0) {
     S.claimed = 0u;
     S.claimed1 = 0u;
@@ -2115,6 +2164,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         nv = (uint32_t)__builtin_popcountll(__ballot(lane < nv && cx <= BI));
         const uint32_t rb = lane < nv ? di_rb(x) : 0u;
         my_ob = (lds_u8 *)S.ob[wv] + (wave_incl_scan(rb) - rb);
+        my_rb = rb;
+        HD_CHECK(wave_incl_scan(rb) <= di_obb(IP, BI), 0x206u);
         my_ob32 = (const lds_u32 *)my_ob;
       }
       const bool valid = lane < nv;
@@ -2124,13 +2175,14 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       uint32_t IB, nchunk;
       round_range(R0, A, Z, IB, nchunk);
       const uint32_t IBX = IB - 16u;
-      const LdsIn inp{ibe};
+      const LdsIn inp{ibe HD_LIM(di_ibw(kSpan))};
       // the prefetched chunks (pf) into the staging buffer, byte-swapped
       auto stage_pf = [&](uint32_t nch) {
 #pragma unroll
         for (uint32_t u = 0; u < kPF; ++u) {
           const uint32_t c = lane + WAVE * u;
           if (c < nch) {
+            HD_CHECK(4u * c + 8u <= di_ibw(kSpan), 0x201u);
             u32x4 v;
             v.x = __builtin_bswap32(pf[u].x);
             v.y = __builtin_bswap32(pf[u].y);
@@ -2176,7 +2228,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t bs = 8u * (s - IBX);
       const uint32_t bend = 8u * (min(b, e + 8u) - IBX);
       const uint32_t bstop = last ? bend : 8u * (e - IBX);
-      DISink sk(my_ob);
+      DISink sk(my_ob HD_LIM(my_ob + my_rb));
       // ---- warm-up of the later items: to the first boundary >= 8 s
       uint32_t entry = bs;
       bool dead = false;  // EOS during the warm-up: entry unknown (re-decoded)
@@ -2209,7 +2261,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       for (uint32_t iter = 0; iter <= WAVE + (kMerge ? 1u : 0u); ++iter) {
         if (kMerge && __ballot(run_)) {
           if (run_) {
-            DISink s3(my_ob);
+            DISink s3(my_ob HD_LIM(my_ob + my_rb));
             uint32_t bq = start;
             rr = dd_run<DISink, false, false, SK>(S.T, inp, bq, bstop, bend, s3, INT32_MAX, dmode, &nslow);
             my_exit = rr.failed ? XFAIL : bq;
@@ -2224,7 +2276,7 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
         if (bal == 0) break;
         const bool pred_mism = lane && ((bal >> (lane - 1u)) & 1u);
         if (mism && !pred_mism) {
-          DISink s3(my_ob);
+          DISink s3(my_ob HD_LIM(my_ob + my_rb));
           if (pred == XFAIL || pred == XUNKNOWN || pred == DD_NONE) {
             rr.failed = true;  // the string failed in an earlier item
             rr.at_end = false;
@@ -2256,6 +2308,8 @@ __global__ __launch_bounds__(WAVE * IW) void k_decode_items(const uint8_t *__res
       const uint32_t h1 = wave_incl_max((!valid || k == 0) ? lane + 1u : 0u);
       const uint32_t excl_h = __shfl(Tinc - V, h1 ? h1 - 1u : 0u, 64);
       const uint32_t seg = h1 ? Tinc - excl_h : Tinc + carry_cnt;  // inclusive
+      HD_CHECK(!valid || V <= my_rb, 0x204u);
+      HD_CHECK(!(valid && last) || t0 + i < n, 0x205u);
       if (valid && last)
         dd_finish(S.T, rr.failed, rr.t, rr.win, seg,
                   task_ovf && auto_slot(b - off0, t0 + i + 1u) > dst_cap, t0 + i, status,
@@ -2498,9 +2552,51 @@ static int decode_items(const uint8_t *src, const uint32_t *src_off, uint32_t n,
 
 #endif  // !HD_PART_ENC
 
+#if HD_BOUNDS && !defined(HD_PART_DEC)
+// the report's self-test: lane 5 records site 0x1FF
+__global__ void k_bounds_selftest() { HD_CHECK(threadIdx.x != 5u, 0x1FFu); }
+#endif
+// (HD_BOUNDS) this translation unit's first recorded violation site, or 0;
+// the words are cleared.  0xFFFFFFFF: the copy failed.
+static uint32_t bounds_take_tu() {
+#if HD_BOUNDS
+  uint32_t w[64];
+  if (hipMemcpyFromSymbol(w, HIP_SYMBOL(g_hd_bounds), sizeof(w)) != hipSuccess) return 0xFFFFFFFFu;
+  uint32_t site = 0;
+  for (uint32_t i = 0; i < 64u; ++i)
+    if (!site && w[i]) site = w[i];
+  static const uint32_t zero[64] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_hd_bounds), zero, sizeof(zero)) != hipSuccess) return 0xFFFFFFFFu;
+  return site;
+#else
+  return 0u;
+#endif
+}
+
 extern "C" {
+// each translation unit's violation words (HD_BOUNDS), read by
+// nghttp2_amd_hd__bounds_check (not exported)
+__attribute__((visibility("hidden"))) uint32_t hd_bounds_take_enc(void);
+__attribute__((visibility("hidden"))) uint32_t hd_bounds_take_dec(void);
 
 #ifndef HD_PART_DEC
+__attribute__((visibility("hidden"))) uint32_t hd_bounds_take_enc(void) { return bounds_take_tu(); }
+
+int nghttp2_amd_hd__bounds_check(uint32_t *site) {
+#if HD_BOUNDS
+  if (!site) return NGHTTP2_AMD_ERR_INVALID_ARGUMENT;
+  if (*site == 0x5E1F7E57u) hipLaunchKernelGGL(k_bounds_selftest, dim3(1), dim3(64), 0, 0);
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_rv(e);
+  const uint32_t a = hd_bounds_take_enc(), b = hd_bounds_take_dec();
+  *site = a ? a : b;
+  return 0;
+#else
+  (void)site;
+  return 1;  // the product build: no checks compiled in
+#endif
+}
+
 const char *nghttp2_amd_hd_version(void) { return "nghttp2_amd_hd 0.2.0 gfx950"; }
 
 int nghttp2_amd_hd_huff_tables(void *sym_out, void *dec_out) {
@@ -2646,6 +2742,8 @@ int nghttp2_amd_hd_huff_decode_slots(const uint32_t *src_off, uint32_t n, uint32
 
 #endif  // !HD_PART_DEC
 #ifndef HD_PART_ENC
+__attribute__((visibility("hidden"))) uint32_t hd_bounds_take_dec(void) { return bounds_take_tu(); }
+
 int nghttp2_amd_hd_huff_decode_batch(const uint8_t *src, const uint32_t *src_off,
                                      uint32_t n, uint8_t *dst, const uint32_t *dst_off,
                                      int32_t *status, uint16_t *fstate, uint8_t *flags,
