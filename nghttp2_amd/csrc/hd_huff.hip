@@ -1497,6 +1497,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_DIRECT_KEEP
 #define DD_DIRECT_KEEP 4u  // ... and to keep it on for the round after
 #endif
+#ifndef DD_DPAIR
+#define DD_DPAIR 1  // dd_run: SLOWK 2 as two pairs per loop trip
+#endif
 #ifndef DD_SK64
 #define DD_SK64 1u  // the 64-byte instance (config 5's 30-bit codes everywhere): every pair
 #endif
@@ -1726,9 +1729,10 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // config 2 +0.8 us; per round, on at 4 lanes and kept at 4, config 5
   // 100.9 -> 96.4 with config 2 41.7 -> 41.9, one box, 16 rounds each.)
   uint32_t it = 0, nlong = 0;
-  auto pairs = [&](auto dir) {
+  // one fast pair; slow: this pair may serve a long code (the slow path)
+  auto pair = [&](auto dir, bool slow) {
     constexpr bool kDirect = decltype(dir)::value;
-    while ((int32_t)nq >= nG) {
+    {
       const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
       const uint32_t e1 = T.lut[w >> (32 - TT::BITS)];
       const uint32_t U1 = E_USED(e1);
@@ -1753,9 +1757,36 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
         ls = 0;
       }
       DD_ADV(U1 + U2);
-      ++it;
-      if ((SLOWK == 1u || (it & (SLOWK - 1u)) == 0u) && e2 == 0u && (!kDirect || e1 != 0u))
+      if (slow && e2 == 0u && (!kDirect || e1 != 0u))
         DD_SLOW(); /* (an e1 of 0 stalls e2 too; direct: e1 = 0 was decoded or stopped) */
+    }
+  };
+  auto pairs = [&](auto dir) {
+    constexpr bool kDirect = decltype(dir)::value;
+#if DD_DPAIR
+    if constexpr (SLOWK == 2u && !kDirect) {
+      // SLOWK 2 as two pairs per trip, the second one serving long codes:
+      // the slow-code period is static (no counter parity in SALU) and the
+      // loop's exec-mask bookkeeping is paid once per two pairs (round 6:
+      // config 3 decode 209.9 / 208.6 / 217.4 vs 213.0 / 210.0 / 220.8 us in
+      // three interleaved sets, outputs equal; configs 2 and 5 flat).  A trip
+      // starts only where its second pair keeps the single pair's bound (the
+      // first takes <= 2 BITS bits and serves no long code); the last pairs,
+      // each serving long codes, run one at a time.  (Four pairs per trip,
+      // bound 4 BITS + BITS + 30: 216.1 vs 210.0; the SLOWK 1 loop as two
+      // pairs, bound BITS + 30: config 2 44.0 vs 42.8, config 5 61.9 vs 60.8
+      // -- profiles/r06/ab/ab_pair_trips.log)
+      while ((int32_t)nq - (int32_t)(2 * TT::BITS) >= nG) {
+        pair(dir, false);
+        pair(dir, true);
+      }
+      while ((int32_t)nq >= nG) pair(dir, true);
+      return;
+    }
+#endif
+    while ((int32_t)nq >= nG) {
+      ++it;
+      pair(dir, SLOWK == 1u || (it & (SLOWK - 1u)) == 0u);
     }
   };
   __builtin_amdgcn_s_setprio(1);
