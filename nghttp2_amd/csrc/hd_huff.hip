@@ -1500,6 +1500,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_DPAIR
 #define DD_DPAIR 1  // dd_run: SLOWK 2 as two pairs per loop trip
 #endif
+#ifndef DD_FSTEP
+#define DD_FSTEP 1  // dd_run: fast single steps between the pairs and the careful steps
+#endif
 #ifndef DD_SK64
 #define DD_SK64 1u  // the 64-byte instance (config 5's 30-bit codes everywhere): every pair
 #endif
@@ -1846,6 +1849,29 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
   // branch
   // (the loop-carried flags are VGPR words: as lane-mask bools every merge
   // of them costs SALU in each step)
+#if DD_FSTEP
+  // fast single steps first, while one lookup stays inside the string (bp +
+  // BITS <= bend) and a 2-symbol entry's second code starts before bstop
+  // (its first is <= BITS - 5 bits: bp <= bstop - (BITS - 4)): no stop rules
+  // to predicate, a lane leaves on its own (exec mask), a long code is left
+  // to the careful steps.  The careful steps then only settle the item's
+  // last code or two.  (Round 6: config 3 decode 212.7 / 211.0 vs 214.3 /
+  // 212.4 us, config 2 42.3 / 42.5 vs 43.1 / 43.2, config 5 59.7 / 60.2 vs
+  // 60.3 / 61.0 in two interleaved sets, outputs equal;
+  // profiles/r06/ab/ab_fast_single_steps.log)
+  {
+    const int32_t S = min((int32_t)bstop - (TT::BITS - 4), (int32_t)bend - TT::BITS);
+    int32_t nS = ~(S - 1);  // bp <= S  <=>  (int) nq >= ~(S - 1)
+    while (!failed && (int32_t)nq >= nS) {
+      const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
+      const uint32_t e = T.lut[w >> (32 - TT::BITS)];
+      nS = e ? nS : INT32_MAX;
+      sink.put(e & E_OUT2, E_CNT8(e));  // (e = 0: two junk bytes, no advance)
+      DD_ADV(E_USED(e));
+    }
+    bp = ~nq + 1u;
+  }
+#endif
   uint32_t done = failed, at_end = 0u, tt = 0u, twin = 0u;
   while (__ballot(done == 0u)) {
     const uint32_t w = __builtin_amdgcn_alignbit(A, B, nq);
