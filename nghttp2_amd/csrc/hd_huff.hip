@@ -307,6 +307,9 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 #ifndef EC_INTERIOR
 #define EC_INTERIOR 1  // k_encode: interior rounds store their words without edge tests
 #endif
+#ifndef EC_CNT_UNROLL
+#define EC_CNT_UNROLL 1  // the count's wave loop: two chunk buffers, unrolled by two
+#endif
 #ifndef EC_CNT_PFD
 #define EC_CNT_PFD 2  // k_enc_count: rounds of chunks in flight per wave (4: no faster)
 #endif
@@ -356,21 +359,10 @@ __device__ __forceinline__ uint32_t wave_string_bits(const uint8_t *__restrict__
   const lds_u16 *pr16 = (const lds_u16 *)pr;
   uint32_t Rc = 0, Pa = 0, Pb = 0;
   bool ga = false, gb = false;
-  // chunks are loaded EC_CNT_PFD rounds ahead
-  uint4 q[EC_CNT_PFD];
-#pragma unroll
-  for (uint32_t d = 0; d < EC_CNT_PFD; ++d) {
-    q[d] = make_uint4(0, 0, 0, 0);
-    if (c0 + 64u * d + lane < c_end) q[d] = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u * d + lane) << 4));
-  }
-  for (uint32_t cb = c0; cb < c_end; cb += 64u) {
+  // one round: the 64 chunks from chunk cb, this lane's in qv
+  auto round = [&](uint32_t cb, const uint4 &qv, bool ok) {
     const uint32_t base = cb << 4;
-    const uint32_t wd[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
-#pragma unroll
-    for (uint32_t d = 0; d + 1 < EC_CNT_PFD; ++d) q[d] = q[d + 1];
-    q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
-    if (cb + 64u * EC_CNT_PFD + lane < c_end)
-      q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + base + 1024u * EC_CNT_PFD + 16u * lane);
+    const uint32_t wd[4] = {ok ? qv.x : 0u, ok ? qv.y : 0u, ok ? qv.z : 0u, ok ? qv.w : 0u};
     uint32_t run = 0, pk[8];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -402,7 +394,52 @@ __device__ __forceinline__ uint32_t wave_string_bits(const uint8_t *__restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // every lane loads (a chunk past the wave's bytes at a clamped index,
+  // used as zeros): a load behind a branch that a whole wave may skip makes
+  // the count of loads in flight path-dependent, and the compiler then waits
+  // for all of them (vmcnt(0)) where it needs the oldest
+  const uint32_t c_last = max(c_end, c0 + 1u) - 1u;
+  auto load = [&](uint32_t c, bool &ok) -> uint4 {
+    ok = c < c_end;
+    return *reinterpret_cast<const uint4 *>(src + ((size_t)min(c, c_last) << 4));
+  };
+#if EC_CNT_UNROLL
+  // chunks two rounds ahead, in two buffers the loop (unrolled by two)
+  // alternates: a buffer is reloaded only after its round has used it, so
+  // no register copy of a load in flight makes the round wait for it.
+  // (Round 6: the rolled loop below rotated q[0] <- q[1] each round, and
+  // that copy of the load just issued waited for it, vmcnt(0) -- every
+  // round took a whole memory latency, whatever EC_CNT_PFD was.  Unrolled:
+  // count 37.1 vs 40.9 us on config 3, encode pair 123.4 vs 127.8, config
+  // 2 count 14.9 vs 15.4, outputs equal; profiles/r06/ab/ab_count_unroll.log)
+  bool oka, okb;
+  uint4 qa = load(c0 + lane, oka), qb = load(c0 + 64u + lane, okb);
+  for (uint32_t cb = c0; cb < c_end; cb += 128u) {
+    round(cb, qa, oka);
+    qa = load(cb + 128u + lane, oka);
+    if (cb + 64u >= c_end) break;
+    round(cb + 64u, qb, okb);
+    qb = load(cb + 192u + lane, okb);
   }
+#else
+  // chunks are loaded EC_CNT_PFD rounds ahead
+  uint4 q[EC_CNT_PFD];
+#pragma unroll
+  for (uint32_t d = 0; d < EC_CNT_PFD; ++d) {
+    q[d] = make_uint4(0, 0, 0, 0);
+    if (c0 + 64u * d + lane < c_end) q[d] = *reinterpret_cast<const uint4 *>(src + ((c0 + 64u * d + lane) << 4));
+  }
+  for (uint32_t cb = c0; cb < c_end; cb += 64u) {
+    const uint4 qv = q[0];
+#pragma unroll
+    for (uint32_t d = 0; d + 1 < EC_CNT_PFD; ++d) q[d] = q[d + 1];
+    q[EC_CNT_PFD - 1] = make_uint4(0, 0, 0, 0);
+    if (cb + 64u * EC_CNT_PFD + lane < c_end)
+      q[EC_CNT_PFD - 1] = *reinterpret_cast<const uint4 *>(src + ((cb + 64u * EC_CNT_PFD + lane) << 4));
+    round(cb, qv, true);
+  }
+#endif
   // an end at the last chunk's end (Z on a chunk boundary)
   if (!ga) Pa = Rc;
   if (!gb) Pb = Rc;
