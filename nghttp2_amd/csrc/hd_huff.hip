@@ -304,6 +304,9 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 }
 
 #define ENC_WAVES 4                  // waves per encode workgroup (tile = 256 strings)
+#ifndef EC_STORE4
+#define EC_STORE4 1  // k_encode: an interior round of <= 256 words as four unconditional stores
+#endif
 #ifndef EC_INTERIOR
 #define EC_INTERIOR 1  // k_encode: interior rounds store their words without edge tests
 #endif
@@ -709,7 +712,11 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
   if (threadIdx.x == WG - 1) o_sh[WG] = o_me + E_me;
   __syncthreads();
   if (nstr == 0) return;
-  const uint32_t OA = o_sh[64u * wv], OZ = o_sh[64u * wv + nstr];  // the wave's output bytes
+  // the wave's output bytes (EC_STORE4, the pack: as scalars, so the
+  // round's word bounds and path choices stay scalar)
+  const uint32_t OA = EC_STORE4 && !FR ? __builtin_amdgcn_readfirstlane(o_sh[64u * wv]) : o_sh[64u * wv];
+  const uint32_t OZ = EC_STORE4 && !FR ? __builtin_amdgcn_readfirstlane(o_sh[64u * wv + nstr])
+                                       : o_sh[64u * wv + nstr];
   const uint64_t G0 = 8ull * OA;
   const uint32_t pad_l = sl && (!FR || H_me) ? 8u * Eh_me - bits_me : 0u;  // EOS-prefix bits after string l
   const uint32_t olast_l = o_me + E_me - 1u;             // its last output byte (if E > 0)
@@ -916,25 +923,55 @@ __global__ __launch_bounds__(WG, EC_WPE) void k_encode(const uint8_t *__restrict
     // vs 135.0 us, emit 217.0 vs 223.6, config 2 flat, outputs equal;
     // profiles/r06/ab/ab_pack_interior_rounds.log)
     if (ilo == 0u && ihi >= nst) {
-      for (uint32_t i = lane; i < nst; i += 64u) {
-        const uint32_t v = __builtin_bswap32(img[EC_M + i]);
-        img[EC_M + i] = 0u;
-        *reinterpret_cast<uint32_t *>(dw + 4u * i) = v;
+#if EC_STORE4
+      // (EC_STORE4, the pack: a round of 1..256 words as exactly four store
+      // instructions with no branch -- a lane past the round's words stores
+      // the last word again, read before any word is cleared; the other
+      // store paths end waiting for their stores.  Config 3 encode pair
+      // 120.9 vs 122.9 us, config 2 flat; the string literals' config 2
+      // 69.8 vs 68.0, so not for them; profiles/r06/ab/ab_pack_store4.log)
+      if (EC_STORE4 && !FR && nst - 1u < 256u) {
+        uint32_t v[4], ix[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) {
+          ix[k] = min(lane + 64u * k, nst - 1u);
+          v[k] = __builtin_bswap32(img[EC_M + ix[k]]);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) img[EC_M + ix[k]] = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) *reinterpret_cast<uint32_t *>(dw + 4u * ix[k]) = v[k];
+      } else
+#endif
+      {
+        for (uint32_t i = lane; i < nst; i += 64u) {
+          const uint32_t v = __builtin_bswap32(img[EC_M + i]);
+          img[EC_M + i] = 0u;
+          *reinterpret_cast<uint32_t *>(dw + 4u * i) = v;
+        }
+#if EC_STORE4
+        if (!FR) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this path's stores, counted out
+#endif
       }
     } else
 #endif
-    for (uint32_t i = lane; i < nst; i += 64u) {
-      const uint32_t v = __builtin_bswap32(img[EC_M + i]);
-      img[EC_M + i] = 0u;
-      if (i >= ilo && i < ihi) {
-        *reinterpret_cast<uint32_t *>(dw + 4u * i) = v;
-      } else {
-        const uint64_t ga = 4ull * (WB + i);
-        for (uint32_t y = 0; y < 4u; ++y) {
-          const uint64_t gq = ga + y;
-          if (gq >= OA && gq < OZ) dst[gq] = (uint8_t)(v >> (8u * y));
+    {
+      for (uint32_t i = lane; i < nst; i += 64u) {
+        const uint32_t v = __builtin_bswap32(img[EC_M + i]);
+        img[EC_M + i] = 0u;
+        if (i >= ilo && i < ihi) {
+          *reinterpret_cast<uint32_t *>(dw + 4u * i) = v;
+        } else {
+          const uint64_t ga = 4ull * (WB + i);
+          for (uint32_t y = 0; y < 4u; ++y) {
+            const uint64_t gq = ga + y;
+            if (gq >= OA && gq < OZ) dst[gq] = (uint8_t)(v >> (8u * y));
+          }
         }
       }
+#if EC_STORE4
+      if (!FR) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
     }
     if (first && lane < EC_M) img[lane] = 0u;  // the bytes before A
     if (!FR) {
