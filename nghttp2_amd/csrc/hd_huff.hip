@@ -310,6 +310,9 @@ __global__ __launch_bounds__(WG) void k_scan_apply(uint32_t *__restrict__ offs, 
 #ifndef EC_INTERIOR
 #define EC_INTERIOR 1  // k_encode: interior rounds store their words without edge tests
 #endif
+#ifndef EC_CNT_SPLIT
+#define EC_CNT_SPLIT 1  // the count's in-chunk prefixes in two halves (16-byte lane stride)
+#endif
 #ifndef EC_CNT_UNROLL
 #define EC_CNT_UNROLL 1  // the count's wave loop: two chunk buffers, unrolled by two
 #endif
@@ -376,8 +379,18 @@ __device__ __forceinline__ uint32_t wave_string_bits(const uint8_t *__restrict__
     u32x4 v0, v1;
     v0.x = pk[0]; v0.y = pk[1]; v0.z = pk[2]; v0.w = pk[3];
     v1.x = pk[4]; v1.y = pk[5]; v1.z = pk[6]; v1.w = pk[7];
+#if EC_CNT_SPLIT
+    // (the chunk's first and second 8 prefixes in two halves of pr: lane
+    // strides of 16 bytes, 4-way per 32 lanes -- the least 16-byte stores
+    // can take -- instead of 32 bytes, 8-way.  Round 6: count 34.9 vs 37.0
+    // us on config 3, 14.4 vs 15.2 on config 2, outputs equal;
+    // profiles/r06/ab/ab_count_split_prefixes.log)
+    *(lds_u32x4 *)(pr + 4u * lane) = v0;
+    *(lds_u32x4 *)(pr + 256u + 4u * lane) = v1;
+#else
     *(lds_u32x4 *)(pr + 8u * lane) = v0;
     *(lds_u32x4 *)(pr + 8u * lane + 4u) = v1;
+#endif
     const uint32_t Sinc = wave_incl_scan(run), Sx = Sinc - run;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -386,11 +399,11 @@ __device__ __forceinline__ uint32_t wave_string_bits(const uint8_t *__restrict__
     const uint32_t ra = a_l - base, rb = b_l - base;
     const uint32_t xa = __shfl(Sx, (ra >> 4) & 63u, 64), xb = __shfl(Sx, (rb >> 4) & 63u, 64);
     if (sl && ra < 1024u) {
-      Pa = Rc + xa + pr16[ra];
+      Pa = Rc + xa + pr16[EC_CNT_SPLIT ? ((ra >> 4) << 3) | (ra & 7u) | ((ra & 8u) << 6) : ra];
       ga = true;
     }
     if (sl && rb < 1024u) {
-      Pb = Rc + xb + pr16[rb];
+      Pb = Rc + xb + pr16[EC_CNT_SPLIT ? ((rb >> 4) << 3) | (rb & 7u) | ((rb & 8u) << 6) : rb];
       gb = true;
     }
     Rc += __builtin_amdgcn_readlane(Sinc, 63);
