@@ -1192,8 +1192,15 @@ __device__ __forceinline__ uint32_t long_entry(const TT &T, uint32_t win, uint32
   // zero: win << (n1 + 1), by alignbit so that n1 = 31 gives 0)
   const uint32_t v = T.long1[long_index(win)];
   const uint32_t L = E_USED(v);
+#if DD_SLOWU
+  // (selects, not an early return: no exec-mask branch in the slow path)
+  const bool fits = L <= rem;
+  const uint32_t r = fits ? v & ~E_EOS : v & ~(E_EOS | 0xFFu);
+  return fits && (v & E_EOS) ? 0xFFFFFFFFu : r;
+#else
   if (L <= rem && (v & E_EOS)) return 0xFFFFFFFFu;
   return L <= rem ? v & ~E_EOS : v & ~(E_EOS | 0xFFu);
+#endif
 }
 // The index of a window's code in T.long1 (long_entry's read).
 __device__ __forceinline__ uint32_t long_index(uint32_t win) {
@@ -1608,6 +1615,9 @@ __global__ __launch_bounds__(DEC_NT) void k_decode(const uint8_t *__restrict__ s
 #ifndef DD_FSTEP
 #define DD_FSTEP 1  // dd_run: fast single steps between the pairs and the careful steps
 #endif
+#ifndef DD_SLOWU
+#define DD_SLOWU 1  // dd_run: the pairs' slow path behind a uniform branch, predicated
+#endif
 #ifndef DD_SK64
 #define DD_SK64 1u  // the 64-byte instance (config 5's 30-bit codes everywhere): every pair
 #endif
@@ -1865,8 +1875,34 @@ __device__ __forceinline__ DDRun dd_run(const TT &T, const IN &ib, uint32_t &bp,
         ls = 0;
       }
       DD_ADV(U1 + U2);
+#if DD_SLOWU
+      // (the slow path behind one uniform branch, predicated per lane: the
+      // wave takes it whenever one of its lanes met a long code -- on config
+      // 3's bytes nearly every serving pair -- and the exec-mask save and
+      // restore of a divergent branch cost every time.  Round 6: config 3
+      // decode 213.5 / 207.4 vs 216.3 / 210.3 us, configs 2 and 5 -0.7 /
+      // -0.3 %, outputs equal; profiles/r06/ab/ab_slow_uniform.log)
+      {
+        const bool need = slow && e2 == 0u && (!kDirect || e1 != 0u);
+        if (__ballot(need)) {
+          const uint32_t rem_ = bend - (~nq + 1u);
+          const uint32_t e_ = slow_entry(T, __builtin_amdgcn_alignbit(A, B, nq), rem_);
+          const bool eos_ = need && e_ == 0xFFFFFFFFu;
+          const bool ok_ = need && e_ != 0xFFFFFFFFu && E_L1(e_) <= rem_;
+          failed |= eos_ ? 1u : 0u;
+          nG = (need && !ok_) ? INT32_MAX : nG;
+          const uint32_t ek_ = ok_ ? e_ : 0u;
+          sink.put(ek_ & E_OUT2, E_CNT8(ek_));  // (ek_ = 0: two junk bytes, no advance)
+          const uint32_t U_ = E_USED(ek_);
+          if (SYNC) ls = need ? U_ : ls;
+          DD_ADV(U_);
+          if (nslow) *nslow += need ? 1u : 0u;
+        }
+      }
+#else
       if (slow && e2 == 0u && (!kDirect || e1 != 0u))
         DD_SLOW(); /* (an e1 of 0 stalls e2 too; direct: e1 = 0 was decoded or stopped) */
+#endif
     }
   };
   auto pairs = [&](auto dir) {
